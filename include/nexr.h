@@ -1,0 +1,168 @@
+/*
+ * nexr.h — C ABI of the MI355X-native reduce-copy primitive.
+ *
+ * This is the drop-in boundary for the one hot path of MJChku/nex-nccl this project rebuilds:
+ * the element-wise K-source / M-destination reduce-copy that every collective's payload goes
+ * through (reference: src/device/common_kernel.h:269-349 `reduceCopy`, inner loop
+ * `reduceCopyPacks` :32-267, element arithmetic src/device/reduce_kernel.h:427-592).
+ *
+ * Plain C: pointers, sizes and integer enums only. Every enum value is numerically identical to
+ * the reference so a caller can pass its own ncclDataType_t / ncclDevRedOp_t / ncclResult_t
+ * values straight through.
+ *
+ * Ownership and ordering (reference src/enqueue.cc:1543-1640, src/device/onerank.cc:48-83):
+ *   - the caller owns every buffer; nothing is allocated or freed inside a hot call;
+ *   - device calls are stream-ordered and asynchronous on the given HIP stream (NULL = the
+ *     default stream of the current device); they never synchronise the host;
+ *   - calls are safe concurrently on different devices / streams (no global mutable state apart
+ *     from a per-device launch-geometry cache initialised once per device);
+ *   - errors are returned, never aborted on.
+ */
+#ifndef NEXR_H_
+#define NEXR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NEXR_API __attribute__((visibility("default")))
+
+#define NEXR_VERSION_MAJOR 0
+#define NEXR_VERSION_MINOR 1
+#define NEXR_VERSION_PATCH 0
+
+/* Maximum fan-in / fan-out of one call: srcs[]/dsts[] hold NCCL_MAX_ARITY+1 = 8 entries
+ * (reference src/device/common.h:101-102, src/include/device.h:816,:842-846). */
+#define NEXR_MAX_SRCS 8
+#define NEXR_MAX_DSTS 8
+
+/* Result codes — identical to ncclResult_t (reference src/nccl.h.in:40-48). */
+typedef enum {
+  nexrSuccess = 0,
+  nexrUnhandledCudaError = 1, /* any hipError_t from the runtime */
+  nexrSystemError = 2,
+  nexrInternalError = 3,
+  nexrInvalidArgument = 4,    /* bad K/M/dtype/op/null pointer/unsupported combination */
+  nexrInvalidUsage = 5,
+  nexrRemoteError = 6,
+  nexrInProgress = 7,
+  nexrNumResults = 8
+} nexrResult_t;
+
+/* Data types — identical to ncclDataType_t (reference src/nccl.h.in:278-290). */
+typedef enum {
+  nexrInt8 = 0, nexrChar = 0,
+  nexrUint8 = 1,
+  nexrInt32 = 2, nexrInt = 2,
+  nexrUint32 = 3,
+  nexrInt64 = 4,
+  nexrUint64 = 5,
+  nexrFloat16 = 6, nexrHalf = 6,
+  nexrFloat32 = 7, nexrFloat = 7,
+  nexrFloat64 = 8, nexrDouble = 8,
+  nexrBfloat16 = 9,
+  nexrFloat8e4m3 = 10, /* declared for enum parity; the fork never compiles its fp8 path
+                          (reduce_kernel.h:17 guard), so calls return nexrInvalidArgument */
+  nexrFloat8e5m2 = 11,
+  nexrNumTypes = 12
+} nexrDataType_t;
+
+/* User-level reduction ops — identical to ncclRedOp_t (reference src/nccl.h.in:259-270). */
+typedef enum { nexrSum = 0, nexrProd = 1, nexrMax = 2, nexrMin = 3, nexrAvg = 4, nexrNumOps = 5 } nexrRedOp_t;
+
+/* Device reduction ops — identical to ncclDevRedOp_t (reference src/include/device.h:683-687). */
+typedef enum {
+  nexrDevSum = 0,
+  nexrDevProd = 1,
+  nexrDevMinMax = 2,     /* redOpArg bit 0: 0 = min, 1 = max (reduce_kernel.h:64) */
+  nexrDevPreMulSum = 3,  /* preOp: x * scalar (scalar = raw bits of T in preOpArgs[s]) */
+  nexrDevSumPostDiv = 4, /* integer types only; redOpArg = divisor<<1 | isSigned */
+  nexrNumDevRedOps = 5
+} nexrDevRedOp_t;
+
+/* Mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693). */
+typedef struct {
+  int op;              /* nexrDevRedOp_t */
+  int proxyOp;         /* nexrRedOp_t the user asked for */
+  int scalarArgIsPtr;  /* scalarArg holds a device pointer to the scalar (onerank.cc:32-42) */
+  uint64_t scalarArg;
+} nexrDevRedOpFull;
+
+typedef void* nexrStream_t; /* a hipStream_t; NULL = default stream */
+
+/*
+ * nexrReduceCopy — replaces the device primitive
+ *   reduceCopy<Unroll,RedFn,T,0,MinSrcs,MaxSrcs,0,MinDsts,MaxDsts,PreOpSrcs>(
+ *       thread, nThreads, redArg, preOpArgs, postOp, nSrcs, srcPtrs, nDsts, dstPtrs, nElts)
+ * (reference src/device/common_kernel.h:331-349), called by genericOp at
+ * src/device/prims_simple.h:264,:272,:282,:290 and by oneRankReduce at src/device/onerank.cc:43.
+ *
+ * For every element i in [0, nElts):
+ *   acc = srcs[0][i]              (then acc = acc * preOpArgs[0]   if 0 < nPreOpSrcs, PreMulSum)
+ *   for s in 1..nSrcs-1:
+ *     v = srcs[s][i]              (then v   = v   * preOpArgs[s]   if s < nPreOpSrcs, PreMulSum)
+ *     acc = reduce(acc, v)        (acc is the FIRST operand: reduce_kernel.h:152-168)
+ *   if postOp: acc = acc / divisor                                  (SumPostDiv)
+ *   dsts[d][i] = acc for every d
+ * with the per-type scalar arithmetic of reduce_kernel.h:238-539 (real arithmetic, i.e. the
+ * fork's SKIP_COMP at reduce_kernel.h:432 removed; Min/Max compared at the signedness of
+ * `datatype`). Rounding to T after every step; integer sum/prod wrap modulo 2^bits.
+ *
+ * Device pointers; any alignment; dsts may alias srcs[0] exactly (in-place). nElts == 0 is a
+ * no-op. 1 <= nSrcs <= 8, 1 <= nDsts <= 8, 0 <= nPreOpSrcs <= nSrcs, preOpArgs may be NULL
+ * when nPreOpSrcs == 0.
+ */
+NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                     size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                                     int nPreOpSrcs, const uint64_t* preOpArgs, int postOp,
+                                     nexrStream_t stream);
+
+/*
+ * nexrReduceCopyHost — the same reduce-copy for buffers in HOST memory (the emulated
+ * transport's staging FIFOs, reference src/include/device.h:753-771): copies the K inputs
+ * host->device, runs nexrReduceCopy, copies the M outputs device->host, and synchronises the
+ * stream before returning. Device scratch is taken from a per-device cache grown on demand
+ * (the only call that may allocate). Inputs may be pageable or pinned (pinned is faster).
+ */
+NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                         size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                                         int nPreOpSrcs, const uint64_t* preOpArgs, int postOp,
+                                         nexrStream_t stream);
+
+/*
+ * nexrHostToDevRedOp — replaces hostToDevRedOp (reference src/enqueue.cc:2185-2278) for the
+ * built-in ops: encodes (op, datatype, nRanks) into the device op and its 64-bit argument
+ * (Min/Max xormask, Avg: integer nRanks<<1|signed or float 1/nRanks bit pattern).
+ */
+NEXR_API nexrResult_t nexrHostToDevRedOp(nexrDevRedOpFull* opFull, int op, int datatype, int nRanks);
+
+/*
+ * nexrLaunchOneRank — replaces ncclLaunchOneRank (reference src/device/onerank.cc:48-83,
+ * declared src/include/device.h:1171): the nRanks == 1 all-reduce. Non-PreMulSum ops are a
+ * stream-ordered copy (skipped when dst == src); PreMulSum runs a K=1 reduce-copy with the
+ * scalar pre-op and postOp (onerank.cc:14-45), the scalar loaded from device memory when
+ * redOp.scalarArgIsPtr.
+ */
+NEXR_API nexrResult_t nexrLaunchOneRank(void* dst, const void* src, size_t nElts, nexrDevRedOpFull redOp,
+                                        int datatype, nexrStream_t stream);
+
+/* Bytes per element of a datatype (reference ncclTypeSize), 0 if unknown. */
+NEXR_API size_t nexrTypeSize(int datatype);
+
+/* Human-readable string for a result code (reference ncclGetErrorString). */
+NEXR_API const char* nexrGetErrorString(nexrResult_t result);
+
+/* Packed version: major*10000 + minor*100 + patch. */
+NEXR_API int nexrGetVersion(void);
+
+/* Last HIP error recorded by this thread inside the library (0 if none) — diagnostics only. */
+NEXR_API int nexrGetLastHipError(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEXR_H_ */

@@ -1,0 +1,228 @@
+"""nex-nccl_amd — MI355X-native reduce-copy primitive (host-side mirror of the reference API).
+
+The product is ``libnexr.so`` (C ABI, ``include/nexr.h``) built from ``csrc/`` for gfx950. This
+module is the Python view of that boundary, mirroring the reference's operator interface for the
+path: the device primitive ``reduceCopy`` (src/device/common_kernel.h:331-349), the one-rank
+launcher ``ncclLaunchOneRank`` (src/device/onerank.cc:48-83) and the op encoder
+``hostToDevRedOp`` (src/enqueue.cc:2185-2278). Same argument meaning, same integer enums and
+result codes; failures raise :class:`NexrError` carrying the ``ncclResult_t``-compatible code.
+
+There is no fallback: if ``libnexr.so`` is missing or fails to load, every call raises.
+Import it with ``importlib.import_module("nex-nccl_amd")`` (the directory name has a hyphen).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from typing import Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnexr.so")
+
+MAX_SRCS = 8
+MAX_DSTS = 8
+
+
+class Result(enum.IntEnum):
+    """ncclResult_t values (reference src/nccl.h.in:40-48)."""
+    Success = 0
+    UnhandledCudaError = 1
+    SystemError = 2
+    InternalError = 3
+    InvalidArgument = 4
+    InvalidUsage = 5
+    RemoteError = 6
+    InProgress = 7
+
+
+class DataType(enum.IntEnum):
+    """ncclDataType_t values (reference src/nccl.h.in:278-290)."""
+    Int8 = 0
+    Uint8 = 1
+    Int32 = 2
+    Uint32 = 3
+    Int64 = 4
+    Uint64 = 5
+    Float16 = 6
+    Float32 = 7
+    Float64 = 8
+    Bfloat16 = 9
+    Float8e4m3 = 10
+    Float8e5m2 = 11
+
+
+class RedOp(enum.IntEnum):
+    """ncclRedOp_t built-in values (reference src/nccl.h.in:259-270)."""
+    Sum = 0
+    Prod = 1
+    Max = 2
+    Min = 3
+    Avg = 4
+
+
+class DevRedOp(enum.IntEnum):
+    """ncclDevRedOp_t values (reference src/include/device.h:683-687)."""
+    Sum = 0
+    Prod = 1
+    MinMax = 2
+    PreMulSum = 3
+    SumPostDiv = 4
+
+
+TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Uint32: 4,
+             DataType.Int64: 8, DataType.Uint64: 8, DataType.Float16: 2, DataType.Float32: 4,
+             DataType.Float64: 8, DataType.Bfloat16: 2, DataType.Float8e4m3: 1,
+             DataType.Float8e5m2: 1}
+
+# ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
+ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
+               "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
+
+
+class NexrError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = int(code)
+        try:
+            name = Result(self.code).name
+        except ValueError:
+            name = "Unknown"
+        super().__init__(f"{what}: nexr result {self.code} ({name})" if what else f"nexr result {self.code} ({name})")
+
+
+class DevRedOpFull(ctypes.Structure):
+    """Mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693)."""
+    _fields_ = [("op", ctypes.c_int), ("proxyOp", ctypes.c_int), ("scalarArgIsPtr", ctypes.c_int),
+                ("scalarArg", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libnexr.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NexrError(Result.InternalError,
+                        f"{LIB_PATH} not built (run __graft_entry__.build() or make -C nex-nccl_amd/csrc)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
+    P = ctypes.POINTER
+    for name in ("nexrReduceCopy", "nexrReduceCopyHost"):
+        f = getattr(L, name)
+        f.argtypes = [i32, P(vp), i32, P(vp), sz, i32, i32, u64, i32, P(u64), i32, vp]
+        f.restype = i32
+    L.nexrHostToDevRedOp.argtypes = [P(DevRedOpFull), i32, i32, i32]
+    L.nexrHostToDevRedOp.restype = i32
+    L.nexrLaunchOneRank.argtypes = [vp, vp, sz, DevRedOpFull, i32, vp]
+    L.nexrLaunchOneRank.restype = i32
+    L.nexrTypeSize.argtypes = [i32]
+    L.nexrTypeSize.restype = sz
+    L.nexrGetErrorString.argtypes = [i32]
+    L.nexrGetErrorString.restype = ctypes.c_char_p
+    L.nexrGetVersion.argtypes = []
+    L.nexrGetVersion.restype = i32
+    L.nexrGetLastHipError.argtypes = []
+    L.nexrGetLastHipError.restype = i32
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        extra = ""
+        if rc == Result.UnhandledCudaError:
+            extra = f" (hipError {lib().nexrGetLastHipError()})"
+        raise NexrError(rc, what + extra)
+
+
+def _ptr_array(ptrs: Sequence[int]):
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = ctypes.c_void_p(int(p)) if p else None
+    return arr
+
+
+def _u64_array(vals: Optional[Sequence[int]]):
+    if not vals:
+        return None
+    arr = (ctypes.c_uint64 * len(vals))()
+    for i, v in enumerate(vals):
+        arr[i] = int(v) & 0xFFFFFFFFFFFFFFFF
+    return arr
+
+
+def reduce_copy_ptrs(srcs: Sequence[int], dsts: Sequence[int], n_elts: int, datatype: int, dev_red_op: int,
+                     red_op_arg: int = 0, pre_op_args: Optional[Sequence[int]] = None, post_op: bool = False,
+                     stream: int = 0, host: bool = False) -> None:
+    """Raw-pointer reduce-copy through the C ABI (``nexrReduceCopy`` / ``nexrReduceCopyHost``).
+
+    ``srcs``/``dsts`` are device addresses (host addresses when ``host=True``); ``stream`` is a
+    hipStream_t handle (0 = default stream). Mirrors reduceCopy(…, redArg, preOpArgs, postOp,
+    nSrcs, srcPtrs, nDsts, dstPtrs, nElts) (common_kernel.h:331-349)."""
+    L = lib()
+    pre = list(pre_op_args) if pre_op_args else []
+    f = L.nexrReduceCopyHost if host else L.nexrReduceCopy
+    rc = f(len(srcs), _ptr_array(srcs), len(dsts), _ptr_array(dsts), int(n_elts), int(datatype),
+           int(dev_red_op), int(red_op_arg) & 0xFFFFFFFFFFFFFFFF, len(pre), _u64_array(pre),
+           1 if post_op else 0, ctypes.c_void_p(int(stream)) if stream else None)
+    _check(rc, "nexrReduceCopyHost" if host else "nexrReduceCopy")
+
+
+def host_to_dev_red_op(op: int, datatype: int, n_ranks: int = 1) -> DevRedOpFull:
+    """hostToDevRedOp (reference src/enqueue.cc:2185-2278) for the built-in ops."""
+    out = DevRedOpFull()
+    _check(lib().nexrHostToDevRedOp(ctypes.byref(out), int(op), int(datatype), int(n_ranks)), "nexrHostToDevRedOp")
+    return out
+
+
+def launch_one_rank(dst: int, src: int, n_elts: int, red_op: DevRedOpFull, datatype: int, stream: int = 0) -> None:
+    """ncclLaunchOneRank (reference src/device/onerank.cc:48-83)."""
+    _check(lib().nexrLaunchOneRank(ctypes.c_void_p(int(dst)) if dst else None,
+                                   ctypes.c_void_p(int(src)) if src else None, int(n_elts), red_op,
+                                   int(datatype), ctypes.c_void_p(int(stream)) if stream else None),
+           "nexrLaunchOneRank")
+
+
+def version() -> int:
+    return lib().nexrGetVersion()
+
+
+# ---- torch convenience layer (device memory and streams only; the compute is libnexr) ----------
+def torch_datatype(dtype) -> DataType:
+    import torch
+    m = {torch.int8: DataType.Int8, torch.uint8: DataType.Uint8, torch.int32: DataType.Int32,
+         torch.int64: DataType.Int64, torch.float16: DataType.Float16, torch.float32: DataType.Float32,
+         torch.float64: DataType.Float64, torch.bfloat16: DataType.Bfloat16}
+    for name, dt in (("uint32", DataType.Uint32), ("uint64", DataType.Uint64)):
+        t = getattr(torch, name, None)
+        if t is not None:
+            m[t] = dt
+    if dtype not in m:
+        raise NexrError(Result.InvalidArgument, f"unsupported torch dtype {dtype}")
+    return m[dtype]
+
+
+def reduce_copy(srcs, dsts, dev_red_op: int = DevRedOp.Sum, red_op_arg: int = 0,
+                pre_op_args: Optional[Sequence[int]] = None, post_op: bool = False, datatype: Optional[int] = None,
+                stream=None) -> None:
+    """Reduce-copy over torch tensors on one device: every dst[i] = fold(srcs)[i].
+
+    All tensors must be contiguous with the same element count. ``datatype`` defaults to the
+    tensors' dtype (pass ``DataType.Uint32``/``Uint64`` explicitly for unsigned views of int32/int64
+    storage). ``stream`` is a torch stream (default: the current stream)."""
+    import torch
+    if not srcs:
+        raise NexrError(Result.InvalidArgument, "no sources")
+    n = srcs[0].numel()
+    for t in list(srcs) + list(dsts):
+        if not t.is_contiguous() or t.numel() != n:
+            raise NexrError(Result.InvalidArgument, "tensors must be contiguous and equally sized")
+    dt = torch_datatype(srcs[0].dtype) if datatype is None else DataType(datatype)
+    if stream is None and srcs[0].is_cuda:
+        stream = torch.cuda.current_stream(srcs[0].device)
+    handle = stream.cuda_stream if stream is not None else 0
+    reduce_copy_ptrs([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], n, dt, dev_red_op,
+                     red_op_arg, pre_op_args, post_op, handle, host=not srcs[0].is_cuda)

@@ -1,0 +1,378 @@
+// nexr_api.cpp — the C ABI (include/nexr.h): argument validation, datatype/op dispatch, launch
+// geometry, the host-staged variant and the op encoder. Host code only; the kernels live in
+// nexr_kernels.hip (one object per datatype).
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <stdlib.h>
+#include <atomic>
+#include <mutex>
+
+#include "nexr_internal.h"
+
+namespace nexr {
+namespace {
+
+thread_local int tLastHipError = 0;
+
+inline nexrResult_t hipFail(hipError_t e) {
+  tLastHipError = (int)e;
+  return nexrUnhandledCudaError;
+}
+#define NEXR_HIP(call)                          \
+  do {                                          \
+    hipError_t e_ = (call);                     \
+    if (e_ != hipSuccess) return hipFail(e_);   \
+  } while (0)
+
+size_t typeSize(int dt) {
+  switch (dt) {
+    case nexrInt8: case nexrUint8: case nexrFloat8e4m3: case nexrFloat8e5m2: return 1;
+    case nexrFloat16: case nexrBfloat16: return 2;
+    case nexrInt32: case nexrUint32: case nexrFloat32: return 4;
+    case nexrInt64: case nexrUint64: case nexrFloat64: return 8;
+  }
+  return 0;
+}
+bool isInteger(int dt) { return dt >= nexrInt8 && dt <= nexrUint64; }
+bool isSignedInt(int dt) { return dt == nexrInt8 || dt == nexrInt32 || dt == nexrInt64; }
+
+// ---- per-device launch geometry, initialised once per device ---------------------------------
+constexpr int kMaxDevices = 64;
+struct DevInfo {
+  std::once_flag once;
+  int cus = 256;
+};
+DevInfo gDev[kMaxDevices];
+
+long envLong(const char* name, long dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtol(v, nullptr, 0);
+}
+
+// Grid: enough workgroups for every CU to hold 8 of them (32 waves/CU), grid-stride beyond.
+// Non-temporal policy: on when the call streams more bytes than the Infinity Cache can keep
+// (NEXR_NT_MIN_BYTES, default 64 MiB). Both overridable for sweeps (NEXR_GRID, NEXR_NT).
+nexrResult_t pickGeometry(uint64_t workItems, uint64_t streamBytes, Geometry* g) {
+  int dev = 0;
+  NEXR_HIP(hipGetDevice(&dev));
+  if (dev >= 0 && dev < kMaxDevices) {
+    DevInfo& di = gDev[dev];
+    std::call_once(di.once, [&] {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+        di.cus = cus;
+    });
+  }
+  const int cus = (dev >= 0 && dev < kMaxDevices) ? gDev[dev].cus : 256;
+  static const long gridOverride = envLong("NEXR_GRID", 0);
+  static const long wgPerCu = envLong("NEXR_WG_PER_CU", 8);
+  static const long ntOverride = envLong("NEXR_NT", -1);
+  static const long ntMinBytes = envLong("NEXR_NT_MIN_BYTES", 64l << 20);
+  uint64_t cap = (uint64_t)cus * (uint64_t)(wgPerCu > 0 ? wgPerCu : 8);
+  uint64_t need = (workItems + kBlock - 1) / kBlock;
+  if (need < 1) need = 1;
+  g->grid = (int)(need < cap ? need : cap);
+  if (gridOverride > 0) g->grid = (int)gridOverride;
+  g->nt = ntOverride >= 0 ? (ntOverride != 0) : (streamBytes >= (uint64_t)ntMinBytes);
+  return nexrSuccess;
+}
+
+hipError_t launchDt(int dt, const RCParams& p, int op, int nSrcs, const Geometry& g, hipStream_t s) {
+  switch (dt) {
+    case 0: return launch_dt0(p, op, nSrcs, g, s);
+    case 1: return launch_dt1(p, op, nSrcs, g, s);
+    case 2: return launch_dt2(p, op, nSrcs, g, s);
+    case 3: return launch_dt3(p, op, nSrcs, g, s);
+    case 4: return launch_dt4(p, op, nSrcs, g, s);
+    case 5: return launch_dt5(p, op, nSrcs, g, s);
+    case 6: return launch_dt6(p, op, nSrcs, g, s);
+    case 7: return launch_dt7(p, op, nSrcs, g, s);
+    case 8: return launch_dt8(p, op, nSrcs, g, s);
+    case 9: return launch_dt9(p, op, nSrcs, g, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// Shared validation for every reduce-copy entry point (error convention: SURVEY §8(b)).
+nexrResult_t validate(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                      int datatype, int op, uint64_t redOpArg, int nPreOpSrcs, const uint64_t* preOpArgs) {
+  if (nSrcs < 1 || nSrcs > NEXR_MAX_SRCS) return nexrInvalidArgument;
+  if (nDsts < 0 || nDsts > NEXR_MAX_DSTS) return nexrInvalidArgument;
+  if (datatype < 0 || datatype >= nexrNumTypes) return nexrInvalidArgument;
+  if (datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
+  if (op < 0 || op >= nexrNumDevRedOps) return nexrInvalidArgument;
+  // SumPostDiv kernels exist for integer types only (generate.py:108 required_cuda).
+  if (op == nexrDevSumPostDiv && !isInteger(datatype)) return nexrInvalidArgument;
+  if (op == nexrDevSumPostDiv && isSignedInt(datatype)) {
+    // The signed quotient divides by the divisor truncated to T (reduce_kernel.h:94): a
+    // divisor that truncates to 0 would divide by zero.
+    uint32_t divisor = (uint32_t)(redOpArg >> 1);
+    if (divisor == 0) divisor = 1;
+    size_t sz = typeSize(datatype);
+    if (sz == 1 && (int8_t)divisor == 0) return nexrInvalidArgument;
+  }
+  if (nPreOpSrcs < 0 || nPreOpSrcs > nSrcs) return nexrInvalidArgument;
+  if (nPreOpSrcs > 0 && preOpArgs == nullptr) return nexrInvalidArgument;
+  if (nElts == 0 || nDsts == 0) return nexrSuccess;
+  if (srcs == nullptr || (nDsts > 0 && dsts == nullptr)) return nexrInvalidArgument;
+  for (int s = 0; s < nSrcs; s++)
+    if (srcs[s] == nullptr) return nexrInvalidArgument;
+  for (int d = 0; d < nDsts; d++)
+    if (dsts[d] == nullptr) return nexrInvalidArgument;
+  return nexrSuccess;
+}
+
+// Split [0, nElts) into head edge / 16-B aligned body / tail edge (RCParams comment).
+void planLayout(RCParams& p, int nSrcs, size_t esz) {
+  uintptr_t phase = (uintptr_t)p.src[0] & 15;
+  bool common = (phase % esz) == 0;
+  for (int s = 1; s < nSrcs && common; s++) common = (((uintptr_t)p.src[s]) & 15) == phase;
+  for (int d = 0; d < p.nDsts && common; d++) common = (((uintptr_t)p.dst[d]) & 15) == phase;
+  if (!common) {
+    p.generic = 1;
+    p.head = 0;
+    p.nPacks = 0;
+    return;
+  }
+  p.generic = 0;
+  uint64_t head = phase ? (16 - phase) / esz : 0;
+  if (head > p.nElts) head = p.nElts;
+  p.head = head;
+  p.nPacks = (p.nElts - head) * esz / 16;
+}
+
+nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                              size_t nElts, int datatype, int op, uint64_t redOpArg, int nPreOpSrcs,
+                              const uint64_t* preOpArgs, const void* prePtr, int postOp, hipStream_t stream) {
+  nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, op, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != nexrSuccess) return r;
+  if (nElts == 0 || nDsts == 0) return nexrSuccess;  // common_kernel.h:288-289: nothing to store
+  const size_t esz = typeSize(datatype);
+  RCParams p;
+  memset(&p, 0, sizeof(p));
+  for (int s = 0; s < nSrcs; s++) p.src[s] = (const char*)srcs[s];
+  for (int d = 0; d < nDsts; d++) p.dst[d] = (char*)dsts[d];
+  for (int s = 0; s < nPreOpSrcs; s++) p.pre[s] = preOpArgs[s];
+  p.prePtr = prePtr;
+  p.redArg = redOpArg;
+  p.nElts = nElts;
+  p.nDsts = nDsts;
+  p.nPreOp = nPreOpSrcs;
+  p.postOp = postOp ? 1 : 0;
+  planLayout(p, nSrcs, esz);
+  Geometry g;
+  const uint64_t items = p.generic ? p.nElts : (p.nPacks + unroll_for(nSrcs) - 1) / unroll_for(nSrcs);
+  r = pickGeometry(items, (uint64_t)(nSrcs + nDsts) * nElts * esz, &g);
+  if (r != nexrSuccess) return r;
+  NEXR_HIP(launchDt(datatype, p, op, nSrcs, g, stream));
+  return nexrSuccess;
+}
+
+// ---- host-staged variant: per-thread, per-device scratch -------------------------------------
+struct Scratch {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int device = -1;
+};
+thread_local Scratch tScratch[8];
+
+nexrResult_t scratchFor(size_t bytes, void** out) {
+  int dev = 0;
+  NEXR_HIP(hipGetDevice(&dev));
+  Scratch* sc = nullptr;
+  for (auto& s : tScratch)
+    if (s.device == dev) { sc = &s; break; }
+  if (!sc)
+    for (auto& s : tScratch)
+      if (s.device < 0) { sc = &s; sc->device = dev; break; }
+  if (!sc) return nexrSystemError;
+  if (sc->bytes < bytes) {
+    if (sc->ptr) NEXR_HIP(hipFree(sc->ptr));
+    sc->ptr = nullptr;
+    sc->bytes = 0;
+    NEXR_HIP(hipMalloc(&sc->ptr, bytes));
+    sc->bytes = bytes;
+  }
+  *out = sc->ptr;
+  return nexrSuccess;
+}
+
+// ---- host-side half/bfloat16 rounding used by the op encoder (RNE, NaN -> 0x7fff) ------------
+uint16_t floatToHalfRne(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t a = x & 0x7fffffffu;
+  if (a > 0x7f800000u) return 0x7fffu;
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds to +-inf
+  if (a < 0x33000001u) return (uint16_t)sign;               // <= 2^-25 rounds to 0
+  uint32_t mant, shift;
+  if (a >= 0x38800000u) {  // normal half
+    mant = a - 0x38000000u;
+    shift = 13;
+  } else {  // subnormal half
+    const uint32_t e = a >> 23;
+    mant = (a & 0x7fffffu) | 0x800000u;
+    shift = 126 - e;
+  }
+  uint32_t q = mant >> shift;
+  const uint32_t rem = mant & ((1u << shift) - 1);
+  const uint32_t halfway = 1u << (shift - 1);
+  if (rem > halfway || (rem == halfway && (q & 1))) q++;
+  return (uint16_t)(sign | q);
+}
+uint16_t floatToBf16Rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fffu;
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+}  // namespace
+}  // namespace nexr
+
+using namespace nexr;
+
+extern "C" {
+
+NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                     size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                                     int nPreOpSrcs, const uint64_t* preOpArgs, int postOp,
+                                     nexrStream_t stream) {
+  return reduceCopyDevice(nSrcs, srcs, nDsts, dsts, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs,
+                          preOpArgs, nullptr, postOp, (hipStream_t)stream);
+}
+
+NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                         size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                                         int nPreOpSrcs, const uint64_t* preOpArgs, int postOp,
+                                         nexrStream_t stream) {
+  nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != nexrSuccess) return r;
+  if (nElts == 0 || nDsts == 0) return nexrSuccess;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t bytes = nElts * typeSize(datatype);
+  const size_t slot = (bytes + 255) & ~(size_t)255;
+  void* base = nullptr;
+  r = scratchFor(slot * (size_t)(nSrcs + 1), &base);
+  if (r != nexrSuccess) return r;
+  char* dev = (char*)base;
+  const void* dsrc[NEXR_MAX_SRCS];
+  for (int k = 0; k < nSrcs; k++) {
+    dsrc[k] = dev + slot * k;
+    NEXR_HIP(hipMemcpyAsync((void*)dsrc[k], srcs[k], bytes, hipMemcpyHostToDevice, s));
+  }
+  void* ddst[1] = {dev + slot * nSrcs};
+  r = reduceCopyDevice(nSrcs, dsrc, 1, ddst, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs,
+                       nullptr, postOp, s);
+  if (r != nexrSuccess) return r;
+  for (int d = 0; d < nDsts; d++) NEXR_HIP(hipMemcpyAsync(dsts[d], ddst[0], bytes, hipMemcpyDeviceToHost, s));
+  NEXR_HIP(hipStreamSynchronize(s));
+  return nexrSuccess;
+}
+
+// Restates hostToDevRedOp (reference src/enqueue.cc:2185-2278) for the built-in ops.
+NEXR_API nexrResult_t nexrHostToDevRedOp(nexrDevRedOpFull* opFull, int op, int datatype, int nRanks) {
+  if (opFull == nullptr) return nexrInvalidArgument;
+  const int nbits = 8 * (int)typeSize(datatype);
+  if (nbits <= 0) return nexrInvalidArgument;
+  const uint64_t allBits = ~(uint64_t)0 >> (64 - nbits);
+  const uint64_t signBit = allBits ^ (allBits >> 1);
+  opFull->scalarArgIsPtr = 0;
+  opFull->proxyOp = op;
+  opFull->scalarArg = 0;
+  switch (op) {
+    case nexrSum: opFull->op = nexrDevSum; break;
+    case nexrProd: opFull->op = nexrDevProd; break;
+    case nexrMin:
+    case nexrMax:
+      opFull->op = nexrDevMinMax;
+      if (isSignedInt(datatype)) opFull->scalarArg ^= signBit;
+      opFull->scalarArg ^= (op == nexrMax) ? allBits : 0;
+      break;
+    case nexrAvg: {
+      if (nRanks < 1) return nexrInvalidArgument;
+      uint64_t u64 = 0;
+      switch (datatype) {
+        case nexrInt8: case nexrInt32: case nexrInt64:
+        case nexrUint8: case nexrUint32: case nexrUint64:
+          opFull->op = nexrDevSumPostDiv;
+          u64 = ((uint64_t)nRanks << 1) | (isSignedInt(datatype) ? 1u : 0u);
+          break;
+        case nexrFloat16:
+          opFull->op = nexrDevPreMulSum;
+          u64 = floatToHalfRne((float)(1.0 / nRanks));
+          break;
+        case nexrBfloat16:
+          opFull->op = nexrDevPreMulSum;
+          u64 = floatToBf16Rne((float)(1.0 / nRanks));
+          break;
+        case nexrFloat32: {
+          opFull->op = nexrDevPreMulSum;
+          float f = (float)(1.0 / nRanks);
+          uint32_t b;
+          memcpy(&b, &f, 4);
+          u64 = b;
+          break;
+        }
+        case nexrFloat64: {
+          opFull->op = nexrDevPreMulSum;
+          double f = 1.0 / nRanks;
+          memcpy(&u64, &f, 8);
+          break;
+        }
+        default:  // fp8: the fork compiles this case out (enqueue.cc:2229-2238 guard)
+          return nexrInvalidArgument;
+      }
+      opFull->scalarArg = u64;
+      break;
+    }
+    default:  // user-created ops need a communicator's op table: not part of this boundary
+      return nexrInvalidArgument;
+  }
+  return nexrSuccess;
+}
+
+// Restates ncclLaunchOneRank (reference src/device/onerank.cc:48-83).
+NEXR_API nexrResult_t nexrLaunchOneRank(void* dst, const void* src, size_t nElts, nexrDevRedOpFull redOp,
+                                        int datatype, nexrStream_t stream) {
+  const size_t esz = typeSize(datatype);
+  if (esz == 0) return nexrInvalidArgument;
+  hipStream_t s = (hipStream_t)stream;
+  if (redOp.op != nexrDevPreMulSum) {
+    if (dst != src && nElts > 0) NEXR_HIP(hipMemcpyAsync(dst, src, nElts * esz, hipMemcpyDeviceToDevice, s));
+    return nexrSuccess;
+  }
+  if (datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
+  const void* srcs[1] = {src};
+  void* dsts[1] = {dst};
+  uint64_t arg = redOp.scalarArg;
+  const void* prePtr = redOp.scalarArgIsPtr ? (const void*)(uintptr_t)redOp.scalarArg : nullptr;
+  return reduceCopyDevice(1, srcs, 1, dsts, nElts, datatype, nexrDevPreMulSum, arg, 1, &arg, prePtr,
+                          /*postOp=*/1, s);
+}
+
+NEXR_API size_t nexrTypeSize(int datatype) { return typeSize(datatype); }
+
+NEXR_API const char* nexrGetErrorString(nexrResult_t result) {
+  switch (result) {
+    case nexrSuccess: return "no error";
+    case nexrUnhandledCudaError: return "unhandled HIP error (run with nexrGetLastHipError for details)";
+    case nexrSystemError: return "unhandled system error";
+    case nexrInternalError: return "internal error";
+    case nexrInvalidArgument: return "invalid argument";
+    case nexrInvalidUsage: return "invalid usage";
+    case nexrRemoteError: return "remote process exited or there was a network error";
+    case nexrInProgress: return "operation in progress";
+    default: return "unknown result code";
+  }
+}
+
+NEXR_API int nexrGetVersion(void) {
+  return NEXR_VERSION_MAJOR * 10000 + NEXR_VERSION_MINOR * 100 + NEXR_VERSION_PATCH;
+}
+
+NEXR_API int nexrGetLastHipError(void) { return tLastHipError; }
+
+}  // extern "C"

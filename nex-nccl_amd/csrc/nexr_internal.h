@@ -1,0 +1,54 @@
+// nexr_internal.h — shared between the C-ABI host code (nexr_api.cpp) and the per-datatype
+// kernel objects (nexr_kernels.hip). Not installed; not part of the ABI.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+#include "../../include/nexr.h"
+
+namespace nexr {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes per workgroup
+
+// Launch parameters of one reduce-copy, passed by value as the kernel argument.
+//
+// Element range layout (host computes it, see plan_layout in nexr_api.cpp):
+//   [0, head)                    edge elements before the first 16-B boundary (scalar path)
+//   [head, head + nPacks*EPP)    the aligned body: every src/dst pointer + head*esz is 16-B aligned
+//   [.., nElts)                  tail edge elements (scalar path)
+// When `generic` is set no common alignment exists and every element takes the scalar path.
+struct RCParams {
+  const char* src[NEXR_MAX_SRCS];
+  char* dst[NEXR_MAX_DSTS];
+  uint64_t pre[NEXR_MAX_SRCS];  // raw pre-op scalar bits per src (PreMulSum), reduce_kernel.h:145,:166
+  const void* prePtr;           // if non-null, pre[0] is loaded from this device address (onerank.cc:32-42)
+  uint64_t redArg;              // op argument (MinMax bit 0, SumPostDiv divisor<<1|signed)
+  uint64_t nElts;
+  uint64_t head;                // edge elements before the body
+  uint64_t nPacks;              // 16-B packs in the body
+  int nDsts;
+  int nPreOp;                   // pre-op applies to srcs[s] for s < nPreOp
+  int postOp;
+  int generic;
+};
+
+// Launch geometry chosen by the host.
+struct Geometry {
+  int grid;
+  bool nt;  // non-temporal loads/stores (streaming working sets larger than the MALL)
+};
+
+// One entry point per datatype, defined in the kernel object compiled with -DNEXR_DT=<dt>.
+// Returns hipSuccess or the launch error.
+#define NEXR_DECLARE_LAUNCH(dt) \
+  hipError_t launch_dt##dt(const RCParams& p, int op, int nSrcs, const Geometry& g, hipStream_t s);
+NEXR_DECLARE_LAUNCH(0) NEXR_DECLARE_LAUNCH(1) NEXR_DECLARE_LAUNCH(2) NEXR_DECLARE_LAUNCH(3)
+NEXR_DECLARE_LAUNCH(4) NEXR_DECLARE_LAUNCH(5) NEXR_DECLARE_LAUNCH(6) NEXR_DECLARE_LAUNCH(7)
+NEXR_DECLARE_LAUNCH(8) NEXR_DECLARE_LAUNCH(9)
+#undef NEXR_DECLARE_LAUNCH
+
+// Body packs handled by one workgroup per loop trip, as a function of fan-in K.
+// Chosen so every lane keeps ~8 x 16-B loads in flight (tools/tune_stream.hip sweep).
+__host__ __device__ constexpr int unroll_for(int K) { return K <= 2 ? 4 : (K <= 4 ? 2 : 1); }
+
+}  // namespace nexr

@@ -1,0 +1,356 @@
+/*
+ * nexr_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded (or pthread-sliced) CPU restatement of the reference reduce-copy,
+ * used as the CHECKER for the HIP path: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it. The product (nex-nccl_amd/libnexr.so) never links or calls it.
+ *
+ * What it restates (reference = MJChku/nex-nccl, paths relative to /root/reference):
+ *   - the element loop of reduceCopyPacks, src/device/common_kernel.h:141-237:
+ *       acc = ld(src0)            (+ applyPreOp when 0 < PreOpSrcs, :145-157)
+ *       for s in 1..nSrcs-1: acc = applyReduce(fn, acc, preOp_s?(ld(src_s)))   (:160-206)
+ *       if postOp: acc = applyPostOp(fn, acc)                                   (:208-212)
+ *       st(dst_d, acc) for every d                                               (:214-237)
+ *     with the pack-level ops reduced to their per-element definition
+ *     (Apply_Reduce, src/device/reduce_kernel.h:152-168: acc is the FIRST argument);
+ *   - the scalar arithmetic of src/device/reduce_kernel.h with SKIP_COMP (:432) removed:
+ *       ncclReduceScalar :434-496, ncclAdd/ncclMultiply :238-248 (generic), :329-337 (half),
+ *       :357-367 (bfloat16), ncclDecodeScalar :218-236, :317-321, :340-345,
+ *       FuncMinMax :59-65 (isMin = (arg&1)==0), FuncSumPostDiv::divide :74-98,
+ *       Apply_PreOp<FuncPreMulSum> :498-518, Apply_PostOp<FuncSumPostDiv> :520-539;
+ *   - datatype folding of src/device/generate.py:128-136 (signed sum/prod run on the unsigned
+ *     type; min/max are compared at the user's signedness — upstream-NCCL semantics, which the
+ *     fork's xormask-free FuncMinMax reproduces when instantiated at the signed type; see
+ *     DESIGN.md "Deviations");
+ *   - hostToDevRedOp, src/enqueue.cc:2185-2278 (built-in ops).
+ *
+ * Third-party arithmetic (not in /root/reference): the half/bfloat16 conversions are CUDA 12.8's
+ * host paths of __half2float/__float2half and __bfloat162float/__float2bfloat16_rn
+ * (cuda_fp16.hpp __internal_float2half, cuda_bf16.hpp __internal_float2bfloat16): IEEE-754
+ * round-to-nearest-even, overflow to infinity, subnormals kept, every NaN -> 0x7fff.
+ * They are restated below from that published algorithm.
+ *
+ * Parity pinning: see DESIGN.md §Oracle. The reference cannot be compiled here (its headers need
+ * CUDA's <nv/target>, absent from the image, and the absent NEX runtime), so this file is pinned
+ * by SURVEY.md §8(c)'s known answers from the compiled reference and by independent IEEE
+ * implementations (tests/golden/make_golden.py: numpy float16, torch bfloat16).
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <pthread.h>
+
+/* enum values identical to include/nexr.h (= ncclDataType_t / ncclDevRedOp_t) */
+enum { DT_I8 = 0, DT_U8 = 1, DT_I32 = 2, DT_U32 = 3, DT_I64 = 4, DT_U64 = 5, DT_F16 = 6, DT_F32 = 7,
+       DT_F64 = 8, DT_BF16 = 9, DT_F8E4M3 = 10, DT_F8E5M2 = 11, DT_NUM = 12 };
+enum { OP_SUM = 0, OP_PROD = 1, OP_MINMAX = 2, OP_PREMULSUM = 3, OP_SUMPOSTDIV = 4, OP_NUM = 5 };
+enum { R_OK = 0, R_INVALID = 4 };
+
+size_t oracle_type_size(int dt) {
+  switch (dt) {
+    case DT_I8: case DT_U8: case DT_F8E4M3: case DT_F8E5M2: return 1;
+    case DT_F16: case DT_BF16: return 2;
+    case DT_I32: case DT_U32: case DT_F32: return 4;
+    case DT_I64: case DT_U64: case DT_F64: return 8;
+  }
+  return 0;
+}
+
+/* ---- bit casts --------------------------------------------------------------------------- */
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+
+/* ---- half <-> float (CUDA host path restated) -------------------------------------------- */
+float oracle_half_to_float(uint16_t h) {
+  uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  uint32_t exp = (h >> 10) & 0x1fu;
+  uint32_t man = h & 0x3ffu;
+  if (exp == 0x1f) return u2f(sign | 0x7f800000u | (man << 13)); /* inf / NaN */
+  if (exp == 0) {
+    if (man == 0) return u2f(sign);
+    /* subnormal: value = man * 2^-24, exact in float */
+    float v = (float)man * u2f(0x33800000u); /* 2^-24 */
+    return sign ? -v : v;
+  }
+  return u2f(sign | ((exp + 112u) << 23) | (man << 13));
+}
+
+uint16_t oracle_float_to_half(float f) {
+  uint32_t x = f2u(f);
+  uint32_t sign = (x >> 16) & 0x8000u;
+  uint32_t a = x & 0x7fffffffu;
+  if (a > 0x7f800000u) return 0x7fffu;                       /* NaN -> canonical 0x7fff */
+  if (a == 0x7f800000u) return (uint16_t)(sign | 0x7c00u);   /* inf */
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);   /* >= 65520 rounds to inf */
+  if (a < 0x33000001u) return (uint16_t)sign;                /* <= 2^-25 rounds to 0 */
+  uint32_t mant, shift;
+  if (a >= 0x38800000u) { mant = a - 0x38000000u; shift = 13; }            /* normal half */
+  else { mant = (a & 0x7fffffu) | 0x800000u; shift = 126u - (a >> 23); }    /* subnormal */
+  uint32_t q = mant >> shift;
+  uint32_t rem = mant & ((1u << shift) - 1u);
+  uint32_t halfway = 1u << (shift - 1u);
+  if (rem > halfway || (rem == halfway && (q & 1u))) q++;
+  return (uint16_t)(sign | q);
+}
+
+/* ---- bfloat16 <-> float ------------------------------------------------------------------ */
+float oracle_bf16_to_float(uint16_t b) { return u2f((uint32_t)b << 16); }
+uint16_t oracle_float_to_bf16(float f) {
+  uint32_t u = f2u(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fffu;
+  uint32_t rem = u << 16, q = u >> 16;
+  if (rem > 0x80000000u || (rem == 0x80000000u && (q & 1u))) q++;
+  return (uint16_t)q;
+}
+
+/* ---- one reduce step per type: ncclReduceScalar(fn, current, value) ---------------------- */
+typedef struct {
+  int op;
+  int isMin;              /* FuncMinMax: (arg & 1) == 0 */
+  uint32_t divisor;       /* FuncSumPostDiv: arg >> 1, 0 -> 1 */
+  int isSigned;           /* FuncSumPostDiv: arg & 1 */
+} Fn;
+
+static inline void make_fn(Fn* fn, int op, uint64_t arg) {
+  fn->op = op;
+  fn->isMin = (arg & 1) == 0;
+  fn->divisor = (uint32_t)(arg >> 1);
+  if (fn->divisor == 0) fn->divisor = 1;
+  fn->isSigned = (arg & 1) != 0;
+}
+
+#define MINMAX(isMin, c, v) ((isMin) ? ((v) < (c) ? (v) : (c)) : ((v) > (c) ? (v) : (c)))
+
+/* unsigned-representation integer ops (sum/prod wrap), signed compare where the type is signed */
+#define INT_REDUCE(UT, ST, SIGNED)                                                          \
+  static inline UT red_##UT##_##SIGNED(const Fn* fn, UT c, UT v) {                          \
+    switch (fn->op) {                                                                       \
+      case OP_PROD: return (UT)(c * v);                                                     \
+      case OP_MINMAX:                                                                       \
+        if (SIGNED) { ST sc = (ST)c, sv = (ST)v; return (UT)MINMAX(fn->isMin, sc, sv); }     \
+        return MINMAX(fn->isMin, c, v);                                                     \
+      default: return (UT)(c + v); /* Sum, PreMulSum, SumPostDiv */                         \
+    }                                                                                       \
+  }
+INT_REDUCE(uint8_t, int8_t, 0)
+INT_REDUCE(uint8_t, int8_t, 1)
+INT_REDUCE(uint32_t, int32_t, 0)
+INT_REDUCE(uint32_t, int32_t, 1)
+INT_REDUCE(uint64_t, int64_t, 0)
+INT_REDUCE(uint64_t, int64_t, 1)
+
+/* FuncSumPostDiv::divide (reduce_kernel.h:83-97) */
+static inline uint8_t div_u8(const Fn* fn, uint8_t u) {
+  if (!fn->isSigned) return (uint8_t)((uint32_t)u / fn->divisor);
+  int8_t s = (int8_t)u, d = (int8_t)fn->divisor; /* d != 0: rejected by the callers */
+  return (uint8_t)(int8_t)((int)s / (int)d);
+}
+static inline uint32_t div_u32(const Fn* fn, uint32_t u) {
+  if (!fn->isSigned) return u / fn->divisor;
+  int32_t s = (int32_t)u, d = (int32_t)fn->divisor;
+  if (d == -1) return (uint32_t)0 - u; /* MIN/-1 is undefined in C: wraps, as the GPU does */
+  return (uint32_t)(s / d);
+}
+static inline uint64_t div_u64(const Fn* fn, uint64_t u) {
+  if (!fn->isSigned) return u / (uint64_t)fn->divisor;
+  int64_t s = (int64_t)u, d = (int64_t)fn->divisor;
+  return (uint64_t)(s / d);
+}
+
+static inline float red_f32(const Fn* fn, float c, float v) {
+  switch (fn->op) {
+    case OP_PROD: return c * v;
+    case OP_MINMAX: return MINMAX(fn->isMin, c, v);
+    default: return c + v;
+  }
+}
+static inline double red_f64(const Fn* fn, double c, double v) {
+  switch (fn->op) {
+    case OP_PROD: return c * v;
+    case OP_MINMAX: return MINMAX(fn->isMin, c, v);
+    default: return c + v;
+  }
+}
+/* half / bfloat16: compute in float, convert back after every step (reduce_kernel.h:329-367,
+ * :470-473) */
+static inline uint16_t red_f16(const Fn* fn, uint16_t c, uint16_t v) {
+  float fc = oracle_half_to_float(c), fv = oracle_half_to_float(v), r;
+  switch (fn->op) {
+    case OP_PROD: r = fc * fv; break;
+    case OP_MINMAX: r = MINMAX(fn->isMin, fc, fv); break;
+    default: r = fc + fv;
+  }
+  return oracle_float_to_half(r);
+}
+static inline uint16_t red_bf16(const Fn* fn, uint16_t c, uint16_t v) {
+  float fc = oracle_bf16_to_float(c), fv = oracle_bf16_to_float(v), r;
+  switch (fn->op) {
+    case OP_PROD: r = fc * fv; break;
+    case OP_MINMAX: r = MINMAX(fn->isMin, fc, fv); break;
+    default: r = fc + fv;
+  }
+  return oracle_float_to_bf16(r);
+}
+
+/* ---- the element loop --------------------------------------------------------------------- */
+typedef struct {
+  int nSrcs, nDsts, dt, op, nPreOp, postOp;
+  const void* const* srcs;
+  void* const* dsts;
+  const uint64_t* pre;
+  uint64_t arg;
+  size_t begin, end;
+} Job;
+
+/* LOOP(T, LOAD-REDUCE-...): shared skeleton of common_kernel.h:141-237 per element */
+#define ELEMENT_LOOP(T, PREOP, REDUCE, POSTOP)                                               \
+  do {                                                                                       \
+    const T* const* S = (const T* const*)j->srcs;                                            \
+    T* const* D = (T* const*)j->dsts;                                                        \
+    for (size_t i = j->begin; i < j->end; i++) {                                             \
+      T acc = S[0][i];                                                                       \
+      if (isPreMul && 0 < j->nPreOp) acc = PREOP(acc, 0);                                    \
+      for (int s = 1; s < j->nSrcs; s++) {                                                   \
+        T v = S[s][i];                                                                       \
+        if (isPreMul && s < j->nPreOp) v = PREOP(v, s);                                      \
+        acc = REDUCE(&fn, acc, v);                                                           \
+      }                                                                                      \
+      if (isPostDiv && j->postOp) acc = POSTOP(&fn, acc);                                    \
+      for (int d = 0; d < j->nDsts; d++) D[d][i] = acc;                                      \
+    }                                                                                        \
+  } while (0)
+
+#define NOPOST(fn, x) (x)
+
+static void run_job(const Job* j) {
+  Fn fn;
+  make_fn(&fn, j->op, j->arg);
+  const int isPreMul = j->op == OP_PREMULSUM;
+  const int isPostDiv = j->op == OP_SUMPOSTDIV;
+  /* Apply_PreOp<FuncPreMulSum>: v * ncclDecodeScalar<T>(preOpArgs[s]) */
+#define PRE_U8(x, s) ((uint8_t)((x) * (uint8_t)j->pre[s]))
+#define PRE_U32(x, s) ((uint32_t)((x) * (uint32_t)j->pre[s]))
+#define PRE_U64(x, s) ((uint64_t)((x) * (uint64_t)j->pre[s]))
+#define PRE_F32(x, s) ((x) * u2f((uint32_t)j->pre[s]))
+#define PRE_F64(x, s) ((x) * u2d(j->pre[s]))
+#define PRE_F16(x, s) oracle_float_to_half(oracle_half_to_float(x) * oracle_half_to_float((uint16_t)j->pre[s]))
+#define PRE_BF16(x, s) oracle_float_to_bf16(oracle_bf16_to_float(x) * oracle_bf16_to_float((uint16_t)j->pre[s]))
+  switch (j->dt) {
+    case DT_I8: ELEMENT_LOOP(uint8_t, PRE_U8, red_uint8_t_1, div_u8); break;
+    case DT_U8: ELEMENT_LOOP(uint8_t, PRE_U8, red_uint8_t_0, div_u8); break;
+    case DT_I32: ELEMENT_LOOP(uint32_t, PRE_U32, red_uint32_t_1, div_u32); break;
+    case DT_U32: ELEMENT_LOOP(uint32_t, PRE_U32, red_uint32_t_0, div_u32); break;
+    case DT_I64: ELEMENT_LOOP(uint64_t, PRE_U64, red_uint64_t_1, div_u64); break;
+    case DT_U64: ELEMENT_LOOP(uint64_t, PRE_U64, red_uint64_t_0, div_u64); break;
+    case DT_F32: ELEMENT_LOOP(float, PRE_F32, red_f32, NOPOST); break;
+    case DT_F64: ELEMENT_LOOP(double, PRE_F64, red_f64, NOPOST); break;
+    case DT_F16: ELEMENT_LOOP(uint16_t, PRE_F16, red_f16, NOPOST); break;
+    case DT_BF16: ELEMENT_LOOP(uint16_t, PRE_BF16, red_bf16, NOPOST); break;
+  }
+}
+
+static int check(int nSrcs, int nDsts, int dt, int op, uint64_t arg, int nPreOp, const uint64_t* pre) {
+  if (nSrcs < 1 || nSrcs > 8 || nDsts < 0 || nDsts > 8) return R_INVALID;
+  if (dt < 0 || dt >= DT_NUM || dt == DT_F8E4M3 || dt == DT_F8E5M2) return R_INVALID;
+  if (op < 0 || op >= OP_NUM) return R_INVALID;
+  if (op == OP_SUMPOSTDIV && dt > DT_U64) return R_INVALID;
+  if (op == OP_SUMPOSTDIV && dt == DT_I8) {
+    uint32_t d = (uint32_t)(arg >> 1);
+    if (d == 0) d = 1;
+    if ((int8_t)d == 0) return R_INVALID;
+  }
+  if (nPreOp < 0 || nPreOp > nSrcs || (nPreOp > 0 && !pre)) return R_INVALID;
+  return R_OK;
+}
+
+int oracle_reduce_copy(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                       int datatype, int devRedOp, uint64_t redOpArg, int nPreOpSrcs,
+                       const uint64_t* preOpArgs, int postOp) {
+  int r = check(nSrcs, nDsts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != R_OK) return r;
+  Job j = {nSrcs, nDsts, datatype, devRedOp, nPreOpSrcs, postOp, srcs, dsts, preOpArgs, redOpArg, 0, nElts};
+  run_job(&j);
+  return R_OK;
+}
+
+static void* thread_main(void* a) { run_job((const Job*)a); return NULL; }
+
+/* Same computation sliced over nThreads pthreads (contiguous slices) — the "all cores" CPU
+ * baseline. */
+int oracle_reduce_copy_mt(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                          int datatype, int devRedOp, uint64_t redOpArg, int nPreOpSrcs,
+                          const uint64_t* preOpArgs, int postOp, int nThreads) {
+  int r = check(nSrcs, nDsts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != R_OK) return r;
+  if (nThreads < 1) nThreads = 1;
+  if (nThreads > 256) nThreads = 256;
+  pthread_t th[256];
+  int live[256];
+  Job jobs[256];
+  size_t per = (nElts + (size_t)nThreads - 1) / (size_t)nThreads;
+  per = (per + 63) & ~(size_t)63;
+  for (int t = 0; t < nThreads; t++) {
+    size_t b = per * (size_t)t, e = b + per;
+    live[t] = 0;
+    if (b >= nElts) continue;
+    if (e > nElts) e = nElts;
+    Job j = {nSrcs, nDsts, datatype, devRedOp, nPreOpSrcs, postOp, srcs, dsts, preOpArgs, redOpArg, b, e};
+    jobs[t] = j;
+    if (pthread_create(&th[t], NULL, thread_main, &jobs[t]) == 0) live[t] = 1;
+    else run_job(&jobs[t]);
+  }
+  for (int t = 0; t < nThreads; t++)
+    if (live[t]) pthread_join(th[t], NULL);
+  return R_OK;
+}
+
+/* hostToDevRedOp restated (reference src/enqueue.cc:2185-2278), built-in ops only.
+ * out[0] = devRedOp, out[1] = scalarArg. Returns 0 or 4. */
+int oracle_host_to_dev_redop(int op, int datatype, int nRanks, uint64_t* out) {
+  size_t sz = oracle_type_size(datatype);
+  if (sz == 0) return R_INVALID;
+  int nbits = 8 * (int)sz;
+  uint64_t allBits = ~(uint64_t)0 >> (64 - nbits);
+  uint64_t signBit = allBits ^ (allBits >> 1);
+  int isSigned = datatype == DT_I8 || datatype == DT_I32 || datatype == DT_I64;
+  uint64_t arg = 0;
+  int dop;
+  switch (op) {
+    case 0: dop = OP_SUM; break;
+    case 1: dop = OP_PROD; break;
+    case 2: case 3:
+      dop = OP_MINMAX;
+      if (isSigned) arg ^= signBit;
+      arg ^= (op == 2) ? allBits : 0; /* ncclMax = 2 */
+      break;
+    case 4:
+      if (nRanks < 1) return R_INVALID;
+      if (datatype <= DT_U64) { dop = OP_SUMPOSTDIV; arg = ((uint64_t)nRanks << 1) | (uint64_t)isSigned; }
+      else if (datatype == DT_F16) { dop = OP_PREMULSUM; arg = oracle_float_to_half((float)(1.0 / nRanks)); }
+      else if (datatype == DT_BF16) { dop = OP_PREMULSUM; arg = oracle_float_to_bf16((float)(1.0 / nRanks)); }
+      else if (datatype == DT_F32) { dop = OP_PREMULSUM; arg = f2u((float)(1.0 / nRanks)); }
+      else if (datatype == DT_F64) { double d = 1.0 / nRanks; dop = OP_PREMULSUM; memcpy(&arg, &d, 8); }
+      else return R_INVALID;
+      break;
+    default: return R_INVALID;
+  }
+  out[0] = (uint64_t)dop;
+  out[1] = arg;
+  return R_OK;
+}
+
+/* Coverage of the reference's single-rank PreMulSum kernel (onerank.cc:23-30,:77-78): block b of
+ * bn = min(32, divUp(nElts*esz, 16 KiB)) handles [b*alignUp(nElts/bn, 16/esz), (b+1)*...) clipped
+ * to nElts. Returns how many leading elements the reference writes (DESIGN.md "Deviations"). */
+size_t oracle_onerank_reference_coverage(size_t nElts, int datatype) {
+  size_t esz = oracle_type_size(datatype);
+  if (esz == 0 || nElts == 0) return 0;
+  size_t bytes = nElts * esz;
+  size_t bn = (bytes + (16u << 10) - 1) / (16u << 10);
+  if (bn > 32) bn = 32;
+  size_t epp = 16 / esz;
+  size_t seg = ((nElts / bn) + epp - 1) / epp * epp;
+  size_t cov = bn * seg;
+  return cov < nElts ? cov : nElts;
+}

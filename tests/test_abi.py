@@ -1,0 +1,123 @@
+"""CPU tests of the drop-in boundary (include/nexr.h, nex-nccl_amd/libnexr.so) — no GPU calls.
+
+The library must load, export exactly the symbols the header declares, keep every enum numerically
+identical to the reference, reject bad arguments with ncclInvalidArgument (4) before touching the
+device, and encode ops exactly as hostToDevRedOp does (src/enqueue.cc:2185-2278).
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+import make_golden as mg
+
+HEADER = os.path.join(ROOT, "include", "nexr.h")
+
+
+def _declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"NEXR_API\s+[\w\s\*]+?\b(nexr\w+)\s*\(", text)))
+
+
+def test_header_declares_the_abi(nexr):
+    assert _declared_symbols() == sorted(nexr.ABI_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(nexr):
+    L = nexr.lib()
+    for name in _declared_symbols():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", nexr.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    ours = {s for s in exported if s.startswith("nexr")}
+    assert ours == set(_declared_symbols()), "only the ABI may be exported"
+
+
+def test_enums_match_reference(nexr):
+    # src/nccl.h.in:40-48 (ncclResult_t), :259-270 (ncclRedOp_t), :278-290 (ncclDataType_t),
+    # src/include/device.h:683-687 (ncclDevRedOp_t)
+    assert [int(r) for r in nexr.Result] == list(range(8))
+    assert (nexr.RedOp.Sum, nexr.RedOp.Prod, nexr.RedOp.Max, nexr.RedOp.Min, nexr.RedOp.Avg) == (0, 1, 2, 3, 4)
+    assert [int(d) for d in nexr.DataType] == list(range(12))
+    assert (nexr.DataType.Float16, nexr.DataType.Float32, nexr.DataType.Bfloat16) == (6, 7, 9)
+    assert [int(o) for o in nexr.DevRedOp] == [0, 1, 2, 3, 4]
+    text = open(HEADER).read()
+    for name, val in (("nexrInvalidArgument", 4), ("nexrFloat8e5m2", 11), ("nexrDevSumPostDiv", 4),
+                      ("NEXR_MAX_SRCS", 8), ("NEXR_MAX_DSTS", 8)):
+        assert re.search(rf"\b{name}\s*=?\s*{val}\b", text), name
+
+
+def test_type_size_and_strings(nexr):
+    L = nexr.lib()
+    for dt, sz in nexr.TYPE_SIZE.items():
+        assert L.nexrTypeSize(int(dt)) == sz
+    assert L.nexrTypeSize(12) == 0
+    assert L.nexrGetErrorString(4) == b"invalid argument"
+    assert nexr.version() == 100
+
+
+def _call(nexr, nsrcs=2, ndsts=1, n=16, dt=7, op=0, arg=0, pre=None, srcs=None, dsts=None):
+    L = nexr.lib()
+    s = srcs if srcs is not None else [0x1000 * (i + 1) for i in range(nsrcs)]
+    d = dsts if dsts is not None else [0x100000 * (i + 1) for i in range(ndsts)]
+    sa = (ctypes.c_void_p * 16)(*s)
+    da = (ctypes.c_void_p * 16)(*d)
+    pre = pre or []
+    pa = (ctypes.c_uint64 * 16)(*pre) if pre else None
+    return L.nexrReduceCopy(nsrcs, sa, ndsts, da, n, dt, op, arg, len(pre), pa, 0, None)
+
+
+def test_invalid_arguments_fail_before_the_device(nexr):
+    assert _call(nexr, nsrcs=0) == 4
+    assert _call(nexr, nsrcs=9) == 4
+    assert _call(nexr, ndsts=9) == 4
+    assert _call(nexr, dt=12) == 4
+    assert _call(nexr, dt=10) == 4                     # fp8: the fork compiles the path out
+    assert _call(nexr, op=5) == 4
+    assert _call(nexr, op=4, dt=7) == 4                # SumPostDiv only for integers
+    assert _call(nexr, op=4, dt=0, arg=(256 << 1) | 1) == 4  # divisor truncates to (int8)0
+    assert _call(nexr, srcs=[0x1000, 0]) == 4          # null source
+    assert _call(nexr, dsts=[0]) == 4                  # null destination
+    L = nexr.lib()
+    sa = (ctypes.c_void_p * 2)(0x1000, 0x2000)
+    da = (ctypes.c_void_p * 1)(0x3000)
+    assert L.nexrReduceCopy(2, sa, 1, da, 16, 7, 0, 0, 3, None, 0, None) == 4  # nPreOp > nSrcs
+    assert L.nexrReduceCopy(2, sa, 1, da, 16, 7, 0, 0, 1, None, 0, None) == 4  # preOpArgs NULL
+
+
+def test_empty_calls_are_noops(nexr):
+    # nElts == 0 and nDsts == 0 return success without launching (common_kernel.h:288-289).
+    assert _call(nexr, n=0) == 0
+    assert _call(nexr, ndsts=0) == 0
+
+
+@pytest.mark.parametrize("dt", sorted(mg.DT_NAMES) + [10, 11])
+@pytest.mark.parametrize("op,nranks", [(0, 2), (1, 2), (2, 4), (3, 4), (4, 1), (4, 3), (4, 8), (5, 2)])
+def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):
+    L = nexr.lib()
+    out = nexr.DevRedOpFull()
+    rc = L.nexrHostToDevRedOp(ctypes.byref(out), op, dt, nranks)
+    if op == 5 or (op == 4 and dt in (10, 11)):
+        assert rc == 4
+        return
+    assert rc == 0
+    if dt in (10, 11):  # oracle has no fp8 arithmetic; encoding only
+        bits = 8
+        all_bits = (1 << bits) - 1
+        exp = {0: (0, 0), 1: (1, 0), 2: (2, all_bits), 3: (2, 0)}[op]
+    else:
+        exp = oracle.host_to_dev_red_op(op, dt, nranks)
+    assert (out.op, out.scalarArg) == exp
+    assert out.proxyOp == op and out.scalarArgIsPtr == 0
+
+
+def test_package_fails_loudly_without_library(nexr, monkeypatch, tmp_path):
+    monkeypatch.setattr(nexr, "_lib", None)
+    monkeypatch.setattr(nexr, "LIB_PATH", str(tmp_path / "missing.so"))
+    with pytest.raises(nexr.NexrError):
+        nexr.lib()

@@ -1,0 +1,265 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the golden vectors and the oracle.
+
+Bar: bit-exact for every datatype (float32/float64 NaNs compared by class; half/bfloat16 bit-exact
+including the canonical 0x7fff NaN). Sizes: every golden case, randomised mid-size cases for every
+(datatype, op, K, M), the BASELINE.json configurations at full size, plus the edge cases the
+reference's reduceCopy handles (unaligned heads/tails, pointers with different 16-B phases, byte
+misalignment, in-place, K=M=8, empty calls).
+"""
+import ctypes
+import hashlib
+import threading
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+STORE_NP = mg.STORE
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+def _to_dev(arr: np.ndarray, offset_bytes: int = 0):
+    """Device byte buffer holding arr at byte offset `offset_bytes` (plus guard bytes)."""
+    raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+    buf = torch.full((raw.size + offset_bytes + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    buf[offset_bytes:offset_bytes + raw.size] = torch.from_numpy(raw.copy()).cuda()
+    return buf
+
+
+def run_gpu(nexr, srcs, n_dsts, dt, op, arg=0, pre=None, post=False, src_off=None, dst_off=None, stream=None):
+    n = srcs[0].size
+    esz = mg.np.dtype(STORE_NP[dt]).itemsize
+    src_off = src_off or [0] * len(srcs)
+    dst_off = dst_off or [0] * n_dsts
+    sbufs = [_to_dev(s, o) for s, o in zip(srcs, src_off)]
+    dbufs = [torch.full((n * esz + o + 64,), 0x5A, dtype=torch.uint8, device="cuda") for o in dst_off]
+    handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    nexr.reduce_copy_ptrs([b.data_ptr() + o for b, o in zip(sbufs, src_off)],
+                          [b.data_ptr() + o for b, o in zip(dbufs, dst_off)], n, dt, op, arg, pre, post, handle)
+    torch.cuda.synchronize()
+    outs = []
+    for b, o in zip(dbufs, dst_off):
+        host = b.cpu().numpy()
+        # guard bytes around the output must be untouched
+        assert (host[:o] == 0x5A).all() and (host[o + n * esz:] == 0x5A).all(), "write outside the destination"
+        outs.append(host[o:o + n * esz].view(STORE_NP[dt]).copy())
+    return outs
+
+
+def same(dt, a, b):
+    return mg.canon_bytes(dt, a) == mg.canon_bytes(dt, b)
+
+
+def test_every_golden_vector_on_gpu(nexr, golden_cases, dev):
+    bad = []
+    for i, c in enumerate(golden_cases):
+        srcs = mg.gen_inputs(c["dt"], c["k"], c["n"], c["seed"], c["special"])
+        m = 1 + (i % 3)
+        outs = run_gpu(nexr, srcs, m, c["dt"], c["op"], c["arg"], c["pre"], c["post"])
+        for o in outs:
+            if hashlib.sha256(mg.canon_bytes(c["dt"], o)).hexdigest() != c["sha256"]:
+                bad.append((c["name"], mg.DT_NAMES[c["dt"]], c["k"], c["n"], c["special"], m))
+                break
+    assert not bad, f"{len(bad)} mismatches vs golden, first: {bad[:6]}"
+
+
+OPS = [("sum", mg.SUM), ("prod", mg.PROD), ("min", mg.MINMAX), ("max", mg.MINMAX), ("premulsum", mg.PREMULSUM),
+       ("sumpostdiv", mg.SUMPOSTDIV)]
+
+
+def _case_args(dt, name, op, k, rng):
+    arg, pre, post = 0, None, False
+    if name in ("min", "max"):
+        arg = mg.minmax_arg(dt, name == "max")
+    if name == "premulsum":
+        vals = [0.5, -1.25, 3.0, 0.125, 1.0, -0.75, 2.0, 0.3333333]
+        npre = int(rng.integers(1, k + 1))
+        pre = [mg.float_scalar_bits(dt, vals[s] if dt not in mg.INTS else s * 5 + 3) for s in range(npre)]
+        post = True
+    if name == "sumpostdiv":
+        arg = (int(rng.integers(1, 9)) << 1) | int(dt in (mg.I8, mg.I32, mg.I64))
+        post = True
+    return arg, pre, post
+
+
+@pytest.mark.parametrize("dt", sorted(mg.DT_NAMES))
+def test_matches_oracle_all_ops_k_m(nexr, oracle, dt, dev):
+    rng = np.random.default_rng(dt)
+    for name, op in OPS:
+        if name == "sumpostdiv" and dt not in mg.INTS:
+            continue
+        for k in range(1, 9):
+            n = int(rng.integers(1000, 70000))
+            m = int(rng.choice([1, 2, 3, 8]))
+            arg, pre, post = _case_args(dt, name, op, k, rng)
+            srcs = mg.gen_inputs(dt, k, n, 777 + k * 31 + op, special=True)
+            exp = oracle.reduce_copy(srcs, 1, dt, op, arg, pre, post)[0]
+            for o in run_gpu(nexr, srcs, m, dt, op, arg, pre, post):
+                assert same(dt, o, exp), (name, k, m, n)
+
+
+@pytest.mark.parametrize("dt", [mg.I8, mg.F16, mg.F32, mg.F64, mg.BF16, mg.U64])
+def test_unaligned_heads_tails_and_phases(nexr, oracle, dt, dev):
+    esz = np.dtype(STORE_NP[dt]).itemsize
+    rng = np.random.default_rng(100 + dt)
+    for trial in range(12):
+        k = int(rng.integers(1, 9))
+        m = int(rng.integers(1, 4))
+        n = int(rng.integers(1, 5000))
+        srcs = mg.gen_inputs(dt, k, n, 4242 + trial, special=True)
+        if trial < 4:    # same 16-B phase everywhere: head/body/tail split
+            ph = int(rng.integers(0, 16 // esz)) * esz
+            so, do = [ph] * k, [ph] * m
+        elif trial < 8:  # different element-aligned phases: generic element path
+            so = [int(rng.integers(0, 16 // esz)) * esz for _ in range(k)]
+            do = [int(rng.integers(0, 16 // esz)) * esz for _ in range(m)]
+        else:            # not even element-aligned (the ABI requires no alignment)
+            so = [int(rng.integers(0, 16)) for _ in range(k)]
+            do = [int(rng.integers(0, 16)) for _ in range(m)]
+        op, name = (mg.SUM, "sum") if trial % 2 == 0 else (mg.MINMAX, "max")
+        arg = mg.minmax_arg(dt, True) if name == "max" else 0
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg)[0]
+        for o in run_gpu(nexr, srcs, m, dt, op, arg, src_off=so, dst_off=do):
+            assert same(dt, o, exp), (trial, so, do, n)
+
+
+def test_in_place_dst_aliases_src0(nexr, oracle, dev):
+    dt = mg.F32
+    srcs = mg.gen_inputs(dt, 3, 100003, 5, special=False)
+    exp = oracle.reduce_copy(srcs, 1, dt, mg.SUM)[0]
+    bufs = [torch.from_numpy(s.copy()).cuda() for s in srcs]
+    nexr.reduce_copy(bufs, [bufs[0]], mg.SUM)
+    torch.cuda.synchronize()
+    assert same(dt, bufs[0].cpu().numpy(), exp)
+
+
+def test_torch_layer_and_streams(nexr, oracle, dev):
+    s = torch.cuda.Stream()
+    a = torch.randn(1 << 20, device="cuda")
+    b = torch.randn(1 << 20, device="cuda")
+    o = torch.empty_like(a)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        nexr.reduce_copy([a, b], [o], nexr.DevRedOp.Sum)
+    s.synchronize()
+    exp = oracle.reduce_copy([a.cpu().numpy(), b.cpu().numpy()], 1, mg.F32, mg.SUM)[0]
+    assert same(mg.F32, o.cpu().numpy(), exp)
+
+
+def test_concurrent_callers_on_separate_streams(nexr, oracle, dev):
+    n = 1 << 18
+    jobs = []
+    for t in range(4):
+        srcs = mg.gen_inputs(mg.BF16, 4, n, 9000 + t, special=True)
+        jobs.append((srcs, oracle.reduce_copy(srcs, 1, mg.BF16, mg.SUM)[0]))
+    results = [None] * len(jobs)
+
+    def work(i):
+        st = torch.cuda.Stream()
+        results[i] = run_gpu(nexr, jobs[i][0], 1, mg.BF16, mg.SUM, stream=st)[0]
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    for (srcs, exp), got in zip(jobs, results):
+        assert same(mg.BF16, got, exp)
+
+
+def test_host_staged_variant(nexr, oracle, dev):
+    for dt, op, name in ((mg.F32, mg.SUM, "sum"), (mg.I8, mg.MINMAX, "min"), (mg.F16, mg.PROD, "prod")):
+        srcs = mg.gen_inputs(dt, 2, 262144 + 3, 31 + dt, special=True)
+        arg = mg.minmax_arg(dt, False) if name == "min" else 0
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg)[0]
+        dsts = [np.zeros_like(srcs[0]) for _ in range(2)]
+        nexr.reduce_copy_ptrs([s.ctypes.data for s in srcs], [d.ctypes.data for d in dsts], srcs[0].size, dt, op,
+                              arg, host=True)
+        for d in dsts:
+            assert same(dt, d, exp)
+
+
+def test_one_rank_launcher(nexr, oracle, dev):
+    for dt in (mg.F32, mg.F16, mg.BF16, mg.F64, mg.I32, mg.U8):
+        n = 131073  # a size where the reference's own grid split leaves a tail unwritten
+        src = mg.gen_inputs(dt, 1, n, 55 + dt, special=True)[0]
+        red = nexr.host_to_dev_red_op(nexr.RedOp.Avg, dt, 4)
+        if dt in mg.INTS:  # integer Avg is SumPostDiv -> a plain copy on one rank (onerank.cc:50-55)
+            assert red.op == nexr.DevRedOp.SumPostDiv
+            exp = src
+        else:
+            assert red.op == nexr.DevRedOp.PreMulSum
+            exp = oracle.reduce_copy([src], 1, dt, mg.PREMULSUM, red.scalarArg, [red.scalarArg], True)[0]
+        s = _to_dev(src)
+        d = torch.zeros_like(s)
+        nexr.launch_one_rank(d.data_ptr(), s.data_ptr(), n, red, dt, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        esz = np.dtype(STORE_NP[dt]).itemsize
+        assert same(dt, d.cpu().numpy()[:n * esz].view(STORE_NP[dt]), exp)
+        # scalarArgIsPtr: the scalar is read from device memory (onerank.cc:32-42)
+        if red.op == nexr.DevRedOp.PreMulSum:
+            sc = torch.tensor([red.scalarArg], dtype=torch.int64).cuda()
+            red2 = nexr.DevRedOpFull(red.op, red.proxyOp, 1, sc.data_ptr())
+            d2 = torch.zeros_like(s)
+            nexr.launch_one_rank(d2.data_ptr(), s.data_ptr(), n, red2, dt, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert same(dt, d2.cpu().numpy()[:n * esz].view(STORE_NP[dt]), exp)
+
+
+def _full_size_check(nexr, oracle, dt, k, n, op, arg, threads=16):
+    """Full-size BASELINE configuration: device-generated inputs, whole output vs the oracle."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + k + dt)
+    esz = np.dtype(STORE_NP[dt]).itemsize
+    if dt in mg.INTS:
+        srcs = [torch.randint(0, 256, (n * esz,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    else:
+        tdt = {mg.F32: torch.float32, mg.F16: torch.float16, mg.BF16: torch.bfloat16}[dt]
+        srcs = [(torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt).view(torch.uint8) for _ in range(k)]
+    dst = torch.empty(n * esz, dtype=torch.uint8, device="cuda")
+    nexr.reduce_copy_ptrs([s.data_ptr() for s in srcs], [dst.data_ptr()], n, dt, op, arg, None, False,
+                          torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    host = [s.cpu().numpy().view(STORE_NP[dt]) for s in srcs]
+    exp = oracle.reduce_copy(host, 1, dt, op, arg, threads=threads)[0]
+    got = dst.cpu().numpy().view(STORE_NP[dt])
+    assert same(dt, got, exp)
+
+
+def test_config_c2_fp32_sum_k2_256mib(nexr, oracle, dev):
+    _full_size_check(nexr, oracle, mg.F32, 2, 64 << 20, mg.SUM, 0)
+
+
+@pytest.mark.parametrize("dt", [mg.F16, mg.BF16])
+def test_config_c3_16bit_sum_k8_256mib(nexr, oracle, dt, dev):
+    _full_size_check(nexr, oracle, dt, 8, 128 << 20, mg.SUM, 0)
+
+
+@pytest.mark.parametrize("dt", [mg.I32, mg.I8])
+@pytest.mark.parametrize("name", ["min", "max", "prod"])
+def test_config_c4_int_sweep_k4_64mib(nexr, oracle, dt, name, dev):
+    esz = np.dtype(STORE_NP[dt]).itemsize
+    op = mg.PROD if name == "prod" else mg.MINMAX
+    arg = mg.minmax_arg(dt, name == "max") if op == mg.MINMAX else 0
+    _full_size_check(nexr, oracle, dt, 4, (64 << 20) // esz, op, arg)
+
+
+def test_large_integer_sum_checksum_property(nexr, dev):
+    # size-independent property at 1 GiB per buffer: sum of the output == sum of the input sums
+    # (mod 2^64), computed on the device by torch independently of the kernel.
+    n = (1 << 30) // 8
+    a = torch.randint(-(1 << 62), 1 << 62, (n,), dtype=torch.int64, device="cuda")
+    b = torch.randint(-(1 << 62), 1 << 62, (n,), dtype=torch.int64, device="cuda")
+    o = torch.empty_like(a)
+    nexr.reduce_copy([a, b], [o], nexr.DevRedOp.Sum)
+    torch.cuda.synchronize()
+    assert int(o.sum()) == int(a.sum() + b.sum())
+    assert torch.equal(o, a + b)
