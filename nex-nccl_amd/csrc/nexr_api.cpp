@@ -4,8 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <stdlib.h>
-#include <atomic>
-#include <mutex>
 
 #include "nexr_internal.h"
 
@@ -36,45 +34,30 @@ size_t typeSize(int dt) {
 bool isInteger(int dt) { return dt >= nexrInt8 && dt <= nexrUint64; }
 bool isSignedInt(int dt) { return dt == nexrInt8 || dt == nexrInt32 || dt == nexrInt64; }
 
-// ---- per-device launch geometry, initialised once per device ---------------------------------
-constexpr int kMaxDevices = 64;
-struct DevInfo {
-  std::once_flag once;
-  int cus = 256;
-};
-DevInfo gDev[kMaxDevices];
-
 long envLong(const char* name, long dflt) {
   const char* v = getenv(name);
   if (!v || !*v) return dflt;
   return strtol(v, nullptr, 0);
 }
 
-// Grid: enough workgroups for every CU to hold 8 of them (32 waves/CU), grid-stride beyond.
-// Non-temporal policy: on when the call streams more bytes than the Infinity Cache can keep
-// (NEXR_NT_MIN_BYTES, default 64 MiB). Both overridable for sweeps (NEXR_GRID, NEXR_NT).
+// Grid: one workgroup per kBlock*U-pack trip ("one-shot"), capped at 2^24 workgroups beyond
+// which the kernel grid-strides. Policy by the bytes the call streams (every src read once, every
+// dst written once): plain below NEXR_NT_LOAD_MIN_BYTES (64 MiB: the data likely sits in L2/MALL
+// and the consumer wants the output there too), non-temporal loads above it, non-temporal loads
+// and stores above NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3)
+// and NEXR_GRID override for sweeps.
 nexrResult_t pickGeometry(uint64_t workItems, uint64_t streamBytes, Geometry* g) {
-  int dev = 0;
-  NEXR_HIP(hipGetDevice(&dev));
-  if (dev >= 0 && dev < kMaxDevices) {
-    DevInfo& di = gDev[dev];
-    std::call_once(di.once, [&] {
-      int cus = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-        di.cus = cus;
-    });
-  }
-  const int cus = (dev >= 0 && dev < kMaxDevices) ? gDev[dev].cus : 256;
   static const long gridOverride = envLong("NEXR_GRID", 0);
-  static const long wgPerCu = envLong("NEXR_WG_PER_CU", 8);
-  static const long ntOverride = envLong("NEXR_NT", -1);
-  static const long ntMinBytes = envLong("NEXR_NT_MIN_BYTES", 64l << 20);
-  uint64_t cap = (uint64_t)cus * (uint64_t)(wgPerCu > 0 ? wgPerCu : 8);
+  static const long polOverride = envLong("NEXR_POLICY", -1);
+  static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);
+  static const long ntStoreMin = envLong("NEXR_NT_STORE_MIN_BYTES", 512l << 20);
+  const uint64_t cap = 1ull << 24;
   uint64_t need = (workItems + kBlock - 1) / kBlock;
   if (need < 1) need = 1;
   g->grid = (int)(need < cap ? need : cap);
   if (gridOverride > 0) g->grid = (int)gridOverride;
-  g->nt = ntOverride >= 0 ? (ntOverride != 0) : (streamBytes >= (uint64_t)ntMinBytes);
+  if (polOverride >= 0) g->pol = polOverride == 0 ? 0 : (polOverride == 1 ? 1 : 3);
+  else g->pol = streamBytes >= (uint64_t)ntStoreMin ? 3 : (streamBytes >= (uint64_t)ntLoadMin ? 1 : 0);
   return nexrSuccess;
 }
 

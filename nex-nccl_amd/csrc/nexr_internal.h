@@ -35,7 +35,7 @@ struct RCParams {
 // Launch geometry chosen by the host.
 struct Geometry {
   int grid;
-  bool nt;  // non-temporal loads/stores (streaming working sets larger than the MALL)
+  int pol;  // cache policy: 0 plain, 1 non-temporal loads, 3 non-temporal loads and stores
 };
 
 // One entry point per datatype, defined in the kernel object compiled with -DNEXR_DT=<dt>.
@@ -47,8 +47,10 @@ NEXR_DECLARE_LAUNCH(4) NEXR_DECLARE_LAUNCH(5) NEXR_DECLARE_LAUNCH(6) NEXR_DECLAR
 NEXR_DECLARE_LAUNCH(8) NEXR_DECLARE_LAUNCH(9)
 #undef NEXR_DECLARE_LAUNCH
 
-// Body packs handled by one workgroup per loop trip, as a function of fan-in K.
-// Chosen so every lane keeps ~8 x 16-B loads in flight (tools/tune_stream.hip sweep).
-__host__ __device__ constexpr int unroll_for(int K) { return K <= 2 ? 4 : (K <= 4 ? 2 : 1); }
+// Packs per lane per source in one workgroup trip (the trip covers kBlock*U packs = 16 KiB per
+// buffer). Steady-state sweeps over U in {1,2,4,8} x block in {256,512,1024} for K = 2, 4, 8
+// (tools/tune_kernel.hip, profiles/r01_tune_*.log): U = 4 with 256-thread blocks is best or
+// within noise of best for every K.
+__host__ __device__ constexpr int unroll_for(int) { return 4; }
 
 }  // namespace nexr

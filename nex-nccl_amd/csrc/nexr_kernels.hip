@@ -5,11 +5,13 @@
 // reduceCopyPacks :141-253) with the real per-type arithmetic of src/device/reduce_kernel.h
 // (:238-539, SKIP_COMP at :432 removed). How it computes it is MI355X-first:
 //   - one 16-B load per lane per source per pack (global_load_dwordx4), 64-lane waves,
-//     4 waves per workgroup, grid-stride over groups of kBlock*U packs so that every lane keeps
-//     ~8 loads in flight (U = unroll_for(K));
+//     4 waves per workgroup; each workgroup owns one 16 KiB trip of every buffer (U = 4 packs
+//     per lane, "one-shot" grid of nPacks/(256*4) workgroups; a grid-stride loop only beyond
+//     2^24 workgroups), so every lane has 4*K independent loads in flight;
 //   - all K source loads of a trip are issued before the first reduce step;
-//   - non-temporal loads and stores for working sets larger than the 256 MiB Infinity Cache
-//     (measured +25 % on the K=2 fp32 stream: tools/tune_stream.hip, profiles/);
+//   - cache policy by working-set size: non-temporal loads once a call streams more than
+//     64 MiB, non-temporal loads AND stores beyond 512 MiB (2x the Infinity Cache) —
+//     steady-state sweeps in tools/tune_kernel.hip / tools/hbm_ceiling.hip, DESIGN.md §Kernel;
 //   - no LDS and no cross-lane traffic: every output element depends only on the same index of
 //     the inputs, so the reference's warp-32 hunk layout (common_kernel.h:94-113) is irrelevant
 //     to the result and is not reproduced.
@@ -192,18 +194,24 @@ template <> struct Ty<nexrBfloat16> {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Memory access
+// Memory access: explicit global (address_space 1) pointers so every access is a global_load /
+// global_store with a 64-bit VGPR address (never flat, never via scratch).
 // ---------------------------------------------------------------------------------------------
-template <bool NT>
+typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+// Cache policy POL: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
+enum { kPolPlain = 0, kPolNtLoad = 1, kPolNtStore = 2, kPolNt = 3 };
+template <int POL>
 __device__ __forceinline__ u32x4 ld16(const char* p) {
-  const u32x4* q = reinterpret_cast<const u32x4*>(p);
-  if constexpr (NT) return __builtin_nontemporal_load(q);
+  g_cu32x4* q = (g_cu32x4*)(p);
+  if constexpr (POL & kPolNtLoad) return __builtin_nontemporal_load(q);
   else return *q;
 }
-template <bool NT>
+template <int POL>
 __device__ __forceinline__ void st16(char* p, u32x4 v) {
-  u32x4* q = reinterpret_cast<u32x4*>(p);
-  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  g_u32x4* q = (g_u32x4*)(p);
+  if constexpr (POL & kPolNtStore) __builtin_nontemporal_store(v, q);
   else *q = v;
 }
 
@@ -260,24 +268,27 @@ struct Fold {
 };
 
 // One element through the same pack arithmetic (lanes other than 0 hold zeros and are dropped).
+// Byte-wise copies: the ABI allows pointers that are not even element-aligned.
 template <int D, int OP, int K, bool IsMin>
-__device__ __noinline__ void do_element(const RCParams& p, const Fold<D, OP, K, IsMin>& f, uint64_t i) {
+__device__ __forceinline__ void do_element(const char* const (&src)[K], char* const (&dst)[NEXR_MAX_DSTS], int nDsts,
+                                           const Fold<D, OP, K, IsMin>& f, uint64_t i) {
   constexpr int esz = 16 / Ty<D>::EPP;
   u32x4 in[K];
 #pragma unroll
   for (int s = 0; s < K; s++) {
     in[s] = (u32x4)0u;
-    __builtin_memcpy(&in[s], p.src[s] + i * esz, esz);
+    __builtin_memcpy(&in[s], src[s] + i * esz, esz);
   }
   u32x4 out = f.run(in);
-  for (int d = 0; d < p.nDsts; d++) __builtin_memcpy(p.dst[d] + i * esz, &out, esz);
+#pragma unroll
+  for (int d = 0; d < NEXR_MAX_DSTS; d++)
+    if (d < nDsts) __builtin_memcpy(dst[d] + i * esz, &out, esz);
 }
 
-template <int D, int OP, int K, bool NT, bool IsMin>
+template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
 __device__ __forceinline__ void body(const RCParams& p) {
   using T = Ty<D>;
   constexpr int esz = 16 / T::EPP;
-  constexpr int U = unroll_for(K);
   Fold<D, OP, K, IsMin> f(p);
   if constexpr (OP == nexrDevPreMulSum) {
     if (p.prePtr) {  // scalarArgIsPtr (onerank.cc:32-42): the scalar lives in device memory
@@ -286,74 +297,83 @@ __device__ __forceinline__ void body(const RCParams& p) {
       f.factor[0] = T::splat(raw);
     }
   }
-  const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t nthreads = (uint64_t)gridDim.x * kBlock;
+  const char* src[K];
+#pragma unroll
+  for (int s = 0; s < K; s++) src[s] = p.src[s];
+  char* dst[NEXR_MAX_DSTS];
+#pragma unroll
+  for (int d = 0; d < NEXR_MAX_DSTS; d++) dst[d] = p.dst[d];
+  const int nDsts = p.nDsts;
+  const uint64_t gid = (uint64_t)blockIdx.x * B + threadIdx.x;
+  const uint64_t nthreads = (uint64_t)gridDim.x * B;
 
   if (p.generic) {  // pointers share no 16-B phase: every element on the scalar path
-    for (uint64_t i = gid; i < p.nElts; i += nthreads) do_element<D, OP, K, IsMin>(p, f, i);
+    for (uint64_t i = gid; i < p.nElts; i += nthreads) do_element<D, OP, K, IsMin>(src, dst, nDsts, f, i);
     return;
   }
   // Edge elements before/after the aligned body: at most 2*(16/esz - 1) of them.
   const uint64_t bodyElts = p.nPacks * T::EPP;
-  const uint64_t tail = p.nElts - p.head - bodyElts;
-  if (gid < p.head) do_element<D, OP, K, IsMin>(p, f, gid);
-  else if (gid < p.head + tail) do_element<D, OP, K, IsMin>(p, f, p.head + bodyElts + (gid - p.head));
+  const uint64_t head = p.head;
+  const uint64_t tail = p.nElts - head - bodyElts;
+  if (gid < head + tail) {
+    const uint64_t e = gid < head ? gid : head + bodyElts + (gid - head);
+    do_element<D, OP, K, IsMin>(src, dst, nDsts, f, e);
+  }
 
-  const char* src[K];
+  // Aligned body: base pointers advanced past the head edge.
 #pragma unroll
-  for (int s = 0; s < K; s++) src[s] = p.src[s] + p.head * esz;
-  char* dst[NEXR_MAX_DSTS];
+  for (int s = 0; s < K; s++) src[s] += head * esz;
 #pragma unroll
-  for (int d = 0; d < NEXR_MAX_DSTS; d++) dst[d] = p.dst[d] + p.head * esz;
-  const int nDsts = p.nDsts;
+  for (int d = 0; d < NEXR_MAX_DSTS; d++) dst[d] += head * esz;
   const uint64_t nPacks = p.nPacks;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock * U;
-
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock * U + threadIdx.x; i < nPacks; i += stride) {
-    if (i + (uint64_t)(U - 1) * kBlock < nPacks) {
-      u32x4 in[U][K];
+  const uint64_t nFull = nPacks / (B * U);  // groups of B*U packs
+  uint64_t g = blockIdx.x;
+  // Full groups: K*U 16-B loads in flight per lane, then the fold, then M*U stores.
+  for (; g < nFull; g += gridDim.x) {
+    const uint64_t off = (g * (B * U) + threadIdx.x) * 16;
+    u32x4 in[U][K];
 #pragma unroll
-      for (int s = 0; s < K; s++)
+    for (int s = 0; s < K; s++)
 #pragma unroll
-        for (int u = 0; u < U; u++) in[u][s] = ld16<NT>(src[s] + (i + (uint64_t)u * kBlock) * 16);
-      u32x4 out[U];
+      for (int u = 0; u < U; u++) in[u][s] = ld16<POL>(src[s] + off + u * B * 16);
+    u32x4 out[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) out[u] = f.run(in[u]);
+    for (int u = 0; u < U; u++) out[u] = f.run(in[u]);
 #pragma unroll
-      for (int d = 0; d < NEXR_MAX_DSTS; d++) {
-        if (d < nDsts) {
+    for (int d = 0; d < NEXR_MAX_DSTS; d++) {
+      if (d < nDsts) {
 #pragma unroll
-          for (int u = 0; u < U; u++) st16<NT>(dst[d] + (i + (uint64_t)u * kBlock) * 16, out[u]);
-        }
-      }
-    } else {
-      for (int u = 0; u < U; u++) {
-        const uint64_t j = i + (uint64_t)u * kBlock;
-        if (j >= nPacks) break;
-        u32x4 in[K];
-#pragma unroll
-        for (int s = 0; s < K; s++) in[s] = ld16<NT>(src[s] + j * 16);
-        u32x4 out = f.run(in);
-        for (int d = 0; d < nDsts; d++) st16<NT>(dst[d] + j * 16, out);
+        for (int u = 0; u < U; u++) st16<POL>(dst[d] + off + u * B * 16, out[u]);
       }
     }
   }
+  // Remaining packs (< B*U): one pack per thread.
+  for (uint64_t j = nFull * (B * U) + gid; j < nPacks; j += nthreads) {
+    u32x4 in[K];
+#pragma unroll
+    for (int s = 0; s < K; s++) in[s] = ld16<POL>(src[s] + j * 16);
+    u32x4 out = f.run(in);
+#pragma unroll
+    for (int d = 0; d < NEXR_MAX_DSTS; d++)
+      if (d < nDsts) st16<POL>(dst[d] + j * 16, out);
+  }
 }
 
-template <int D, int OP, int K, bool NT>
-__global__ __launch_bounds__(kBlock) void reduce_copy_kernel(RCParams p) {
+template <int D, int OP, int K, int POL, int U = unroll_for(K), int B = kBlock>
+__global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
   if constexpr (OP == nexrDevMinMax) {
-    if ((p.redArg & 1) == 0) body<D, OP, K, NT, true>(p);  // isMin = (arg&1)==0, reduce_kernel.h:64
-    else body<D, OP, K, NT, false>(p);
+    if ((p.redArg & 1) == 0) body<D, OP, K, POL, true, U, B>(p);  // isMin = (arg&1)==0, reduce_kernel.h:64
+    else body<D, OP, K, POL, false, U, B>(p);
   } else {
-    body<D, OP, K, NT, false>(p);
+    body<D, OP, K, POL, false, U, B>(p);
   }
 }
 
 template <int D, int OP, int K>
 static hipError_t launch_k(const RCParams& p, const Geometry& g, hipStream_t s) {
-  const void* fn = g.nt ? (const void*)&reduce_copy_kernel<D, OP, K, true>
-                        : (const void*)&reduce_copy_kernel<D, OP, K, false>;
+  const void* fn = g.pol == kPolNt       ? (const void*)&reduce_copy_kernel<D, OP, K, kPolNt>
+                   : g.pol == kPolNtLoad ? (const void*)&reduce_copy_kernel<D, OP, K, kPolNtLoad>
+                                         : (const void*)&reduce_copy_kernel<D, OP, K, kPolPlain>;
   void* args[] = {const_cast<RCParams*>(&p)};
   return hipLaunchKernel(fn, dim3(g.grid), dim3(kBlock), args, 0, s);
 }
