@@ -175,11 +175,12 @@ def main(argv=None):
     import torch
 
     cfg = CONFIGS[args.config]
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
     dist = Dist("nccl")
     if dist.world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={dist.world}")
-    torch.cuda.set_device(dist.local_rank)
-    dev = torch.device("cuda", dist.local_rank)
     pkg = importlib.import_module("nex-nccl_amd")
     pkg.lib()
 

@@ -1,0 +1,60 @@
+/*
+ * nexr_ring.h — CPU-emulated ring all-reduce that drives the reduce-copy ABI (include/nexr.h)
+ * from the reference's own schedule: the caller side of the drop-in boundary.
+ *
+ * It restates, on host threads (one per emulated rank, 1 channel, SIMPLE protocol):
+ *   - runRing for ncclAllReduce (reference src/device/all_reduce.h:12-84),
+ *   - Primitives::genericOp slicing and the reduceCopy call sites (src/device/prims_simple.h:190-330,
+ *     directSend/directRecvReduceDirectSend/directRecvReduceCopyDirectSend/directRecvCopyDirectSend/
+ *     directRecv :897-976),
+ *   - the FIFO credit protocol of waitPeer/postPeer (prims_simple.h:111-188): NCCL_STEPS = 8 slots of
+ *     buffBytes/8 per connection, head/tail step counters, StepPerSlice = 2, SlicePerChunk = 2
+ *     (src/include/collectives.h:17-18),
+ *   - the host chunking for ring SIMPLE (src/enqueue.cc:1993-1996: chunkSize = stepSize * 4),
+ *   - ncclLaunchOneRank for nRanks == 1 (src/device/onerank.cc:48-83),
+ *   - op encoding through nexrHostToDevRedOp (src/enqueue.cc:2185-2278).
+ * Every reduceCopy site calls a nexrReduceCopyFn — nexrReduceCopyHost (host memory) or
+ * nexrReduceCopy + stream sync (device memory) by default.
+ */
+#ifndef NEXR_RING_H_
+#define NEXR_RING_H_
+
+#include "nexr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same signature as nexrReduceCopy / nexrReduceCopyHost. */
+typedef nexrResult_t (*nexrReduceCopyFn)(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                         size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                                         int nPreOpSrcs, const uint64_t* preOpArgs, int postOp,
+                                         nexrStream_t stream);
+
+typedef enum { nexrRingHostMemory = 0, nexrRingDeviceMemory = 1 } nexrRingMemMode_t;
+
+typedef struct {
+  int nRanks;          /* emulated ranks (threads), >= 1 */
+  size_t buffBytes;    /* per-connection SIMPLE buffer (NCCL_BUFFSIZE); 0 = 4 MiB default */
+  int memMode;         /* nexrRingMemMode_t: where user buffers and FIFOs live */
+  nexrReduceCopyFn fn; /* NULL = nexrReduceCopyHost (host mode) / nexrReduceCopy (device mode) */
+  int timeoutMs;       /* spin-wait bound per FIFO wait; 0 = 60000 */
+} nexrRingConfig;
+
+typedef struct nexrRingComm* nexrRingComm_t;
+
+/* Device mode: rank r uses HIP device r % deviceCount; FIFOs live on the receiving rank's device. */
+NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* comm, const nexrRingConfig* config);
+
+/* ncclAllReduce over all emulated ranks at once: sendbuffs[r] / recvbuffs[r] are rank r's buffers
+ * (host or device memory per memMode; in-place allowed). op is an ncclRedOp_t built-in. */
+NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t count, int datatype, int op);
+
+NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t comm);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEXR_RING_H_ */

@@ -1,0 +1,371 @@
+// nexr_ring.cpp — CPU-emulated ring all-reduce (include/nexr_ring.h): the reference's own
+// collective schedule, restated on host threads, calling the reduce-copy ABI at exactly the
+// reduceCopy sites of Primitives::genericOp. This is the drop-in demonstration for BASELINE
+// configs[0] ("fp32 sum all-reduce, 4 MiB, 2 CPU-emulated ranks"): the schedule is unchanged,
+// only the primitive underneath is the MI355X kernel.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+
+#include "../../include/nexr_ring.h"
+
+namespace {
+
+constexpr int kSteps = 8;                                // NCCL_STEPS (src/include/device.h:649)
+constexpr int kSliceSteps = kSteps / 4;                  // ALLREDUCE_SLICESTEPS (collectives.h:17)
+constexpr int kChunkSteps = kSteps / 2;                  // ALLREDUCE_CHUNKSTEPS (collectives.h:18)
+constexpr int kSlicePerChunk = kChunkSteps / kSliceSteps;
+constexpr size_t kDefaultBuffBytes = 4u << 20;           // NCCL_BUFFSIZE default (init.cc:620-634)
+
+// One directed connection prev -> r. The FIFO belongs to the receiver (the sender writes into it,
+// like a P2P/SHM transport's recv buffer, src/include/device.h:753-771).
+struct Conn {
+  char* fifo = nullptr;
+  alignas(64) std::atomic<uint64_t> tail{0};  // steps published by the sender   (postPeer, Send)
+  alignas(64) std::atomic<uint64_t> head{0};  // steps released by the receiver  (postPeer, Recv)
+};
+
+int64_t divUp(int64_t a, int64_t b) { return (a + b - 1) / b; }
+int64_t alignUp(int64_t a, int64_t b) { return divUp(a, b) * b; }
+
+}  // namespace
+
+struct nexrRingComm {
+  nexrRingConfig cfg;
+  size_t stepBytes = 0;
+  std::vector<Conn*> conns;          // conns[r]: connection into rank r from rank r-1
+  std::vector<uint64_t> recvStep;    // per rank: next step to consume from conns[r]
+  std::vector<uint64_t> sendStep;    // per rank: next step to produce into conns[(r+1)%n]
+  std::vector<int> devices;
+  std::vector<hipStream_t> streams;
+  bool broken = false;
+};
+
+namespace {
+
+struct Shared {
+  std::atomic<bool> abort{false};
+  std::atomic<int> firstError{0};
+  void fail(nexrResult_t r) {
+    int expected = 0;
+    firstError.compare_exchange_strong(expected, (int)r);
+    abort.store(true);
+  }
+};
+
+// One rank's Primitives<T, RedOp, FanSymmetric<1>, 1, ProtoSimple> (prims_simple.h), host side.
+struct Prims {
+  nexrRingComm* c;
+  Shared* sh;
+  int rank;
+  Conn* recvConn;
+  Conn* sendConn;
+  const char* userInput;
+  char* userOutput;
+  size_t esz;
+  int64_t stepSize;  // elements per FIFO step (prims_simple.h:607)
+  int datatype, devOp;
+  uint64_t redOpArgs[1];
+  nexrReduceCopyFn fn;
+  hipStream_t stream;
+  bool device;
+
+  // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
+  // abortable like checkAbort (primitives.h:142-156).
+  bool waitAtLeast(std::atomic<uint64_t>& a, uint64_t target) {
+    if (a.load(std::memory_order_acquire) >= target) return true;
+    const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+    auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 0;; spins++) {
+      if (a.load(std::memory_order_acquire) >= target) return true;
+      if (sh->abort.load(std::memory_order_relaxed)) return false;
+      if ((spins & 1023) == 0 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) {
+        sh->fail(nexrInternalError);
+        return false;
+      }
+      std::this_thread::yield();
+    }
+  }
+
+  // genericOp<DirectRecv=0, DirectSend=0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330),
+  // with the non-direct FIFO pointers (waitPeer :150-164 default branch).
+  bool genericOp(bool Recv, bool Send, bool Src, bool Dst, int64_t srcIx, int64_t dstIx, int64_t nelem,
+                 bool postOp) {
+    nelem = nelem < 0 ? 0 : nelem;
+    int64_t sliceSize = stepSize * kSliceSteps;
+    sliceSize = std::max(divUp(nelem, 16 * kSlicePerChunk) * 16, sliceSize / 32);
+    int64_t offset = 0;
+    for (int slice = 0; slice < kSlicePerChunk; slice++) {
+      sliceSize = std::min(sliceSize, nelem - offset);
+      if (sliceSize < 0) sliceSize = 0;
+      uint64_t& rs = c->recvStep[rank];
+      uint64_t& ss = c->sendStep[rank];
+      const char* recvPtr = nullptr;
+      char* sendPtr = nullptr;
+      if (Recv) {  // wait for the peer's data: tail >= step + StepPerSlice
+        if (!waitAtLeast(recvConn->tail, rs + kSliceSteps)) return false;
+        recvPtr = recvConn->fifo + (rs % kSteps) * c->stepBytes;
+      }
+      if (Send) {  // wait for credit: head + NCCL_STEPS >= step + StepPerSlice
+        if (ss + kSliceSteps > (uint64_t)kSteps && !waitAtLeast(sendConn->head, ss + kSliceSteps - kSteps))
+          return false;
+        sendPtr = sendConn->fifo + (ss % kSteps) * c->stepBytes;
+      }
+      if (sliceSize > 0) {
+        // srcs: local buffer at index 0 (if Src), peers after it; dsts: user output at 0 (if Dst),
+        // next peer after it (prims_simple.h:131-132, :238-242).
+        const void* srcs[2];
+        void* dsts[2];
+        int ns = 0, nd = 0;
+        if (Src) srcs[ns++] = userInput + (srcIx + offset) * esz;
+        if (Recv) srcs[ns++] = recvPtr;
+        if (Dst) dsts[nd++] = userOutput + (dstIx + offset) * esz;
+        if (Send) dsts[nd++] = sendPtr;
+        // PreOpSrcs = SrcBuf != Input ? 0 : 1 (prims_simple.h:279-280); preOpArgs = redOpArgs.
+        const int nPre = Src ? 1 : 0;
+        nexrResult_t r = fn(ns, srcs, nd, dsts, (size_t)sliceSize, datatype, devOp, redOpArgs[0], nPre,
+                            nPre ? redOpArgs : nullptr, postOp ? 1 : 0, (nexrStream_t)stream);
+        if (r == nexrSuccess && device) {
+          hipError_t e = hipStreamSynchronize(stream);  // data complete before the step is posted
+          if (e != hipSuccess) r = nexrUnhandledCudaError;
+        }
+        if (r != nexrSuccess) {
+          sh->fail(r);
+          return false;
+        }
+      }
+      // postPeer (prims_simple.h:177-188): release the slot / publish the data.
+      if (Recv) {
+        rs += kSliceSteps;
+        recvConn->head.store(rs, std::memory_order_release);
+      }
+      if (Send) {
+        ss += kSliceSteps;
+        sendConn->tail.store(ss, std::memory_order_release);
+      }
+      offset += sliceSize;
+    }
+    return true;
+  }
+  bool directSend(int64_t inpIx, int64_t n) { return genericOp(false, true, true, false, inpIx, -1, n, false); }
+  bool directRecvReduceDirectSend(int64_t inpIx, int64_t n) { return genericOp(true, true, true, false, inpIx, -1, n, false); }
+  bool directRecvReduceCopyDirectSend(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
+    return genericOp(true, true, true, true, inpIx, outIx, n, postOp);
+  }
+  bool directRecvCopyDirectSend(int64_t outIx, int64_t n) { return genericOp(true, true, false, true, -1, outIx, n, false); }
+  bool directRecv(int64_t outIx, int64_t n) { return genericOp(true, false, false, true, -1, outIx, n, false); }
+};
+
+// runRing<T, RedOp, ProtoSimple> (all_reduce.h:12-84) for one rank, 1 channel (gridOffset 0,
+// channelCount = count, chunkCount = chunkSize / sizeof(T): enqueue.cc:1993-1996, :655-678).
+void runRing(Prims& p, int nranks, int64_t count) {
+  const int ringIx = p.rank;
+  int64_t chunkCount = (int64_t)(p.c->stepBytes * kChunkSteps / p.esz);
+  const int64_t loopCount = nranks * chunkCount;
+  auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
+  for (int64_t elemOffset = 0; elemOffset < count; elemOffset += loopCount) {
+    const int64_t remCount = count - elemOffset;
+    if (remCount < loopCount) chunkCount = alignUp(divUp(remCount, nranks), 16 / (int64_t)p.esz);
+    auto at = [&](int chunk, int64_t* offset) {
+      const int64_t chunkOffset = chunk * chunkCount;
+      *offset = elemOffset + chunkOffset;
+      return std::min(chunkCount, remCount - chunkOffset);
+    };
+    int64_t offset, nelem;
+    // step 0: push data to next GPU
+    nelem = at(modRanks(ringIx + nranks - 1), &offset);
+    if (!p.directSend(offset, nelem)) return;
+    // k-2 steps: reduce and copy to next GPU
+    for (int j = 2; j < nranks; ++j) {
+      nelem = at(modRanks(ringIx + nranks - j), &offset);
+      if (!p.directRecvReduceDirectSend(offset, nelem)) return;
+    }
+    // step k-1: reduce this buffer and data -> final result, stored and pushed
+    nelem = at(ringIx, &offset);
+    if (!p.directRecvReduceCopyDirectSend(offset, offset, nelem, /*postOp=*/true)) return;
+    // k-2 steps: copy to next GPU
+    for (int j = 1; j < nranks - 1; ++j) {
+      nelem = at(modRanks(ringIx + nranks - j), &offset);
+      if (!p.directRecvCopyDirectSend(offset, nelem)) return;
+    }
+    // final copy from buffer to dest
+    nelem = at(modRanks(ringIx + 1), &offset);
+    if (!p.directRecv(offset, nelem)) return;
+  }
+}
+
+nexrResult_t defaultHostFn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t n, int dt,
+                           int op, uint64_t arg, int nPre, const uint64_t* pre, int post, nexrStream_t s) {
+  return nexrReduceCopyHost(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
+}
+nexrResult_t defaultDeviceFn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t n, int dt,
+                             int op, uint64_t arg, int nPre, const uint64_t* pre, int post, nexrStream_t s) {
+  return nexrReduceCopy(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConfig* cfg) {
+  if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024) return nexrInvalidArgument;
+  if (cfg->memMode != nexrRingHostMemory && cfg->memMode != nexrRingDeviceMemory) return nexrInvalidArgument;
+  auto* c = new nexrRingComm();
+  c->cfg = *cfg;
+  if (c->cfg.buffBytes == 0) c->cfg.buffBytes = kDefaultBuffBytes;
+  if (c->cfg.buffBytes % (kSteps * 16) != 0) {
+    delete c;
+    return nexrInvalidArgument;
+  }
+  if (!c->cfg.fn) c->cfg.fn = cfg->memMode == nexrRingDeviceMemory ? defaultDeviceFn : defaultHostFn;
+  c->stepBytes = c->cfg.buffBytes / kSteps;
+  const int n = cfg->nRanks;
+  c->recvStep.assign(n, 0);
+  c->sendStep.assign(n, 0);
+  c->devices.assign(n, 0);
+  c->streams.assign(n, nullptr);
+  int nDev = 0;
+  if (cfg->memMode == nexrRingDeviceMemory || !cfg->fn) {
+    if (hipGetDeviceCount(&nDev) != hipSuccess || nDev < 1) {
+      delete c;
+      return nexrUnhandledCudaError;
+    }
+  }
+  for (int r = 0; r < n; r++) {
+    c->conns.push_back(new Conn());
+    if (nDev > 0) {
+      c->devices[r] = r % nDev;
+      if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams[r]) != hipSuccess) {
+        nexrRingCommDestroy(c);
+        return nexrUnhandledCudaError;
+      }
+    }
+    if (cfg->memMode == nexrRingDeviceMemory) {
+      if (hipMalloc((void**)&c->conns[r]->fifo, c->cfg.buffBytes) != hipSuccess) {
+        nexrRingCommDestroy(c);
+        return nexrUnhandledCudaError;
+      }
+    } else {
+      c->conns[r]->fifo = (char*)aligned_alloc(4096, c->cfg.buffBytes);
+      if (!c->conns[r]->fifo) {
+        nexrRingCommDestroy(c);
+        return nexrSystemError;
+      }
+    }
+  }
+  if (cfg->memMode == nexrRingDeviceMemory && nDev > 1) {  // sender writes into the receiver's FIFO
+    for (int r = 0; r < n; r++) {
+      int a = c->devices[r], b = c->devices[(r + 1) % n];
+      if (a != b) {
+        (void)hipSetDevice(a);
+        hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          nexrRingCommDestroy(c);
+          return nexrUnhandledCudaError;
+        }
+        (void)hipGetLastError();
+      }
+    }
+  }
+  *out = c;
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t count, int datatype, int op) {
+  if (!c || !sendbuffs || !recvbuffs) return nexrInvalidArgument;
+  if (c->broken) return nexrInvalidUsage;
+  const int n = c->cfg.nRanks;
+  const size_t esz = nexrTypeSize(datatype);
+  if (esz == 0 || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
+  nexrDevRedOpFull red;
+  nexrResult_t r = nexrHostToDevRedOp(&red, op, datatype, n);
+  if (r != nexrSuccess) return r;
+  for (int i = 0; i < n; i++)
+    if (count > 0 && (!sendbuffs[i] || !recvbuffs[i])) return nexrInvalidArgument;
+  if (count == 0) return nexrSuccess;
+  const bool device = c->cfg.memMode == nexrRingDeviceMemory;
+
+  if (n == 1) {  // ncclLaunchOneRank (onerank.cc:48-83)
+    if (device) (void)hipSetDevice(c->devices[0]);
+    if (red.op == nexrDevPreMulSum) {
+      uint64_t arg = red.scalarArg;
+      r = c->cfg.fn(1, sendbuffs, 1, recvbuffs, count, datatype, nexrDevPreMulSum, arg, 1, &arg, 1,
+                    (nexrStream_t)c->streams[0]);
+      if (r == nexrSuccess && device && hipStreamSynchronize(c->streams[0]) != hipSuccess) r = nexrUnhandledCudaError;
+      return r;
+    }
+    if (sendbuffs[0] != recvbuffs[0]) {
+      if (device) {
+        if (hipMemcpy(recvbuffs[0], sendbuffs[0], count * esz, hipMemcpyDeviceToDevice) != hipSuccess)
+          return nexrUnhandledCudaError;
+      } else {
+        memcpy(recvbuffs[0], sendbuffs[0], count * esz);
+      }
+    }
+    return nexrSuccess;
+  }
+
+  Shared sh;
+  std::vector<std::thread> threads;
+  for (int rank = 0; rank < n; rank++) {
+    threads.emplace_back([&, rank] {
+      if (device || c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+      Prims p;
+      p.c = c;
+      p.sh = &sh;
+      p.rank = rank;
+      p.recvConn = c->conns[rank];
+      p.sendConn = c->conns[(rank + 1) % n];
+      p.userInput = (const char*)sendbuffs[rank];
+      p.userOutput = (char*)recvbuffs[rank];
+      p.esz = esz;
+      p.stepSize = (int64_t)(c->stepBytes / esz);
+      p.datatype = datatype;
+      p.devOp = red.op;
+      p.redOpArgs[0] = red.scalarArg;
+      p.fn = c->cfg.fn;
+      p.stream = c->streams[rank];
+      p.device = device;
+      runRing(p, n, (int64_t)count);
+    });
+  }
+  for (auto& t : threads) t.join();
+  if (sh.firstError.load() != 0) {
+    c->broken = true;  // step counters are mid-protocol: the communicator cannot be reused
+    return (nexrResult_t)sh.firstError.load();
+  }
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
+  if (!c) return nexrInvalidArgument;
+  for (size_t r = 0; r < c->conns.size(); r++) {
+    Conn* k = c->conns[r];
+    if (k->fifo) {
+      if (c->cfg.memMode == nexrRingDeviceMemory) {
+        (void)hipSetDevice(c->devices[r]);
+        (void)hipFree(k->fifo);
+      } else {
+        free(k->fifo);
+      }
+    }
+    delete k;
+  }
+  for (size_t r = 0; r < c->streams.size(); r++)
+    if (c->streams[r]) {
+      (void)hipSetDevice(c->devices[r]);
+      (void)hipStreamDestroy(c->streams[r]);
+    }
+  delete c;
+  return nexrSuccess;
+}
+
+}  // extern "C"

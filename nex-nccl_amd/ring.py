@@ -1,0 +1,88 @@
+"""Python view of the CPU-emulated ring all-reduce (include/nexr_ring.h, libnexr_ring.so).
+
+The ring schedule (runRing, src/device/all_reduce.h:12-84) and the genericOp slicing / FIFO credit
+protocol (src/device/prims_simple.h:111-330) run on host threads in C++; every reduceCopy site calls
+the MI355X reduce-copy ABI (or any function with its signature, e.g. a test checker).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+from . import NexrError, Result, _check, lib
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+RING_LIB_PATH = os.path.join(_HERE, "libnexr_ring.so")
+RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingCommDestroy")
+
+HOST_MEMORY = 0
+DEVICE_MEMORY = 1
+
+REDUCE_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
+                                  ctypes.c_void_p)
+
+
+class RingConfig(ctypes.Structure):
+    _fields_ = [("nRanks", ctypes.c_int), ("buffBytes", ctypes.c_size_t), ("memMode", ctypes.c_int),
+                ("fn", ctypes.c_void_p), ("timeoutMs", ctypes.c_int)]
+
+
+_ring = None
+
+
+def ring_lib() -> ctypes.CDLL:
+    global _ring
+    if _ring is None:
+        lib()  # libnexr.so first (the ring library links against it)
+        if not os.path.exists(RING_LIB_PATH):
+            raise NexrError(Result.InternalError, f"{RING_LIB_PATH} not built")
+        L = ctypes.CDLL(RING_LIB_PATH)
+        L.nexrRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(RingConfig)]
+        L.nexrRingCommCreate.restype = ctypes.c_int
+        L.nexrRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.nexrRingAllReduce.restype = ctypes.c_int
+        L.nexrRingCommDestroy.argtypes = [ctypes.c_void_p]
+        L.nexrRingCommDestroy.restype = ctypes.c_int
+        _ring = L
+    return _ring
+
+
+class RingComm:
+    """N emulated ranks (host threads) joined in one ring; `all_reduce` runs ncclAllReduce on all."""
+
+    def __init__(self, n_ranks: int, mem_mode: int = HOST_MEMORY, buff_bytes: int = 0,
+                 fn_address: Optional[int] = None, timeout_ms: int = 0):
+        cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms)
+        h = ctypes.c_void_p()
+        _check(ring_lib().nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
+        self._h = h
+        self.n_ranks = n_ranks
+
+    def all_reduce(self, sendbuffs: Sequence[int], recvbuffs: Sequence[int], count: int, datatype: int,
+                   op: int) -> None:
+        if len(sendbuffs) != self.n_ranks or len(recvbuffs) != self.n_ranks:
+            raise NexrError(Result.InvalidArgument, "one send and one recv buffer per rank")
+        s = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in sendbuffs])
+        r = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in recvbuffs])
+        _check(ring_lib().nexrRingAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrRingAllReduce")
+
+    def close(self) -> None:
+        if self._h:
+            ring_lib().nexrRingCommDestroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

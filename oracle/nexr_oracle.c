@@ -274,6 +274,16 @@ int oracle_reduce_copy(int nSrcs, const void* const* srcs, int nDsts, void* cons
   return R_OK;
 }
 
+/* The same computation with the nexrReduceCopyFn signature (include/nexr_ring.h), so tests can run
+ * the ring schedule on CPU with the oracle underneath (the stream argument is ignored). */
+int oracle_reduce_copy_fn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                          int datatype, int devRedOp, uint64_t redOpArg, int nPreOpSrcs,
+                          const uint64_t* preOpArgs, int postOp, void* stream) {
+  (void)stream;
+  return oracle_reduce_copy(nSrcs, srcs, nDsts, dsts, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs,
+                            preOpArgs, postOp);
+}
+
 static void* thread_main(void* a) { run_job((const Job*)a); return NULL; }
 
 /* Same computation sliced over nThreads pthreads (contiguous slices) — the "all cores" CPU

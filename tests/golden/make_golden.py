@@ -56,7 +56,8 @@ def splitmix64(seed: int, n: int) -> np.ndarray:
 
 
 def f32_to_f16_bits(x: np.ndarray) -> np.ndarray:
-    h = x.astype(np.float32).astype(np.float16).view(np.uint16).copy()
+    with np.errstate(over="ignore", invalid="ignore"):
+        h = x.astype(np.float32).astype(np.float16).view(np.uint16).copy()
     h[np.isnan(x)] = 0x7FFF
     return h
 

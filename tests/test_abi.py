@@ -116,6 +116,21 @@ def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):
     assert out.proxyOp == op and out.scalarArgIsPtr == 0
 
 
+def test_ring_library_exports_its_header():
+    import importlib
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    text = open(os.path.join(ROOT, "include", "nexr_ring.h")).read()
+    declared = sorted(set(re.findall(r"NEXR_API\s+[\w\s\*]+?\b(nexr\w+)\s*\(", text)))
+    assert declared == sorted(ring.RING_ABI_SYMBOLS)
+    L = ring.ring_lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", ring.RING_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line and "nexr" in line}
+    assert exported == set(declared)
+    for name in declared:
+        assert hasattr(L, name)
+
+
 def test_package_fails_loudly_without_library(nexr, monkeypatch, tmp_path):
     monkeypatch.setattr(nexr, "_lib", None)
     monkeypatch.setattr(nexr, "LIB_PATH", str(tmp_path / "missing.so"))

@@ -1,0 +1,59 @@
+"""World-size-2 rehearsal of bench.py's N>1 path on CPU (gloo): every rank processes its own
+independent chunk (no data-path collective), the timed region is bracketed by
+barriers, and the reported time is the MAX over ranks. The per-rank step here is the CPU oracle
+standing in for the device launch (the GPU step itself is covered by tests -m gpu)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    import time
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests", "golden")]
+    import bench
+    import make_golden as mg
+    import oracle
+
+    d = bench.Dist("gloo")
+    srcs = mg.gen_inputs(mg.F32, 2, 50_000, 1000 + rank * 7, special=False)  # rank-own chunk
+    out = [None]
+
+    def step(i):
+        if rank == 1:
+            time.sleep(0.01)  # skew: rank 1 is the slow one
+        out[0] = oracle.reduce_copy(srcs, 1, mg.F32, mg.SUM)[0]
+
+    local, mx = bench.timed_steps(step, steps=5, warmup=1, sync=lambda: None, dist=d)
+    ok = np.array_equal(out[0], (srcs[0] + srcs[1]).astype(np.float32))
+    d.close()
+    q.put((rank, local, mx, ok))
+
+
+def test_two_rank_independent_chunks_max_timer():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = sorted(q.get(timeout=120) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    assert all(p.exitcode == 0 for p in ps)
+    (r0, l0, m0, ok0), (r1, l1, m1, ok1) = res
+    assert ok0 and ok1
+    assert m0 == m1 == max(l0, l1)
+    assert l1 >= 0.05  # the skewed rank's 5 steps

@@ -1,0 +1,106 @@
+"""CPU tests of the emulated ring all-reduce schedule (include/nexr_ring.h).
+
+The C++ driver restates runRing + genericOp + the FIFO credit protocol; here every reduceCopy site
+is served by the CPU oracle (passed in as the nexrReduceCopyFn), so the SCHEDULE is checked without a
+GPU: results must equal oracle/ring.py's independent restatement of the ring's fold order, bit for
+bit, across rank counts, FIFO wrap-around (small buffers, many loops) and every op encoding.
+"""
+import ctypes
+import importlib
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+
+@pytest.fixture(scope="module")
+def ring(nexr):
+    return importlib.import_module("nex-nccl_amd.ring")
+
+
+@pytest.fixture(scope="module")
+def oracle_fn(oracle):
+    return ctypes.cast(oracle.lib().oracle_reduce_copy_fn, ctypes.c_void_p).value
+
+
+def _run(ring, oracle_fn, inputs, dt, op, buff_bytes, in_place=False):
+    n = len(inputs)
+    send = [x.copy() for x in inputs]
+    recv = send if in_place else [np.zeros_like(x) for x in inputs]
+    with ring.RingComm(n, ring.HOST_MEMORY, buff_bytes, oracle_fn, timeout_ms=20000) as comm:
+        comm.all_reduce([a.ctypes.data for a in send], [b.ctypes.data for b in recv], inputs[0].size, dt, op)
+    return recv
+
+
+CASES = [  # (datatype, op ncclRedOp_t, special inputs)
+    (mg.F32, 0, False), (mg.BF16, 0, True), (mg.F16, 4, True), (mg.I32, 3, True), (mg.I32, 2, True),
+    (mg.I8, 4, True), (mg.U64, 1, True), (mg.F64, 4, False), (mg.U8, 2, True), (mg.F32, 1, True),
+]
+
+
+@pytest.mark.parametrize("n_ranks", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("dt,op,special", CASES)
+def test_ring_matches_fold_order_oracle(ring, oracle, oracle_fn, n_ranks, dt, op, special):
+    from oracle.ring import ring_allreduce_expected
+    buff = 64 << 10  # 8 KiB steps: many loops, FIFO wrap-around and credit stalls
+    count = 50_000 + 7 * n_ranks
+    inputs = mg.gen_inputs(dt, n_ranks, count, 0xA11 + 97 * dt + op, special)
+    got = _run(ring, oracle_fn, inputs, dt, op, buff)
+    exp = ring_allreduce_expected(inputs, dt, op, buff)
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, got[r]) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+def test_two_rank_fp32_sum_is_in0_plus_in1(ring, oracle_fn):
+    # BASELINE configs[0] shape (4 MiB per rank, default 4 MiB buffers): out = in0 + in1 on both ranks.
+    inputs = mg.gen_inputs(mg.F32, 2, 1 << 20, 2024, False)
+    got = _run(ring, oracle_fn, inputs, mg.F32, 0, 0)
+    exp = (inputs[0] + inputs[1]).astype(np.float32)
+    for r in range(2):
+        assert np.array_equal(got[r].view(np.uint32), exp.view(np.uint32))
+
+
+@pytest.mark.parametrize("count", [0, 1, 3, 17, 4097])
+def test_ring_small_and_ragged_counts(ring, oracle, oracle_fn, count):
+    from oracle.ring import ring_allreduce_expected
+    inputs = mg.gen_inputs(mg.F32, 3, count, 77, True) if count else [np.zeros(0, np.float32)] * 3
+    got = _run(ring, oracle_fn, inputs, mg.F32, 0, 1 << 14)
+    exp = ring_allreduce_expected(inputs, mg.F32, 0, 1 << 14)
+    for r in range(3):
+        assert mg.canon_bytes(mg.F32, got[r]) == mg.canon_bytes(mg.F32, exp[r])
+
+
+def test_ring_in_place(ring, oracle, oracle_fn):
+    from oracle.ring import ring_allreduce_expected
+    inputs = mg.gen_inputs(mg.I32, 4, 30_001, 5, True)
+    got = _run(ring, oracle_fn, inputs, mg.I32, 0, 1 << 15, in_place=True)
+    exp = ring_allreduce_expected(inputs, mg.I32, 0, 1 << 15)
+    for r in range(4):
+        assert np.array_equal(got[r], exp[r])
+
+
+def test_ring_reuse_comm_across_calls(ring, oracle, oracle_fn):
+    # step counters persist across collectives (FIFO slot = step % NCCL_STEPS)
+    from oracle.ring import ring_allreduce_expected
+    with ring.RingComm(3, ring.HOST_MEMORY, 1 << 14, oracle_fn, timeout_ms=20000) as comm:
+        for it in range(4):
+            inputs = mg.gen_inputs(mg.BF16, 3, 10_000 + 999 * it, 300 + it, True)
+            recv = [np.zeros_like(x) for x in inputs]
+            comm.all_reduce([a.ctypes.data for a in inputs], [b.ctypes.data for b in recv], inputs[0].size, mg.BF16, 0)
+            exp = ring_allreduce_expected(inputs, mg.BF16, 0, 1 << 14)
+            for r in range(3):
+                assert np.array_equal(recv[r], exp[r])
+
+
+def test_ring_rejects_bad_arguments(ring, oracle_fn, nexr):
+    with pytest.raises(nexr.NexrError):
+        ring.RingComm(0, ring.HOST_MEMORY, 0, oracle_fn)
+    with pytest.raises(nexr.NexrError):
+        ring.RingComm(2, ring.HOST_MEMORY, 1000, oracle_fn)  # not a multiple of 8 x 16 B
+    with ring.RingComm(2, ring.HOST_MEMORY, 1 << 14, oracle_fn) as comm:
+        a = np.zeros(16, np.float32)
+        with pytest.raises(nexr.NexrError):
+            comm.all_reduce([a.ctypes.data] * 2, [a.ctypes.data] * 2, 16, 10, 0)  # fp8
+        with pytest.raises(nexr.NexrError):
+            comm.all_reduce([a.ctypes.data] * 2, [a.ctypes.data] * 2, 16, mg.F32, 9)  # user op

@@ -1,0 +1,56 @@
+"""GPU tests of the emulated ring all-reduce with the MI355X reduce-copy underneath (BASELINE
+configs[0]: fp32 sum all-reduce, 4 MiB, 2 CPU-emulated ranks): host-memory mode (every reduceCopy
+site goes through nexrReduceCopyHost, the staging FIFOs stay in host memory) and device-memory mode
+(buffers and FIFOs in HBM, nexrReduceCopy + stream sync per slice)."""
+import importlib
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ring(nexr):
+    assert torch.cuda.is_available()
+    return importlib.import_module("nex-nccl_amd.ring")
+
+
+def test_config_c1_two_ranks_fp32_sum_host_memory(ring):
+    inputs = mg.gen_inputs(mg.F32, 2, 1 << 20, 4242, False)  # 4 MiB per rank
+    recv = [np.zeros_like(x) for x in inputs]
+    with ring.RingComm(2, ring.HOST_MEMORY) as comm:
+        comm.all_reduce([a.ctypes.data for a in inputs], [b.ctypes.data for b in recv], 1 << 20, mg.F32, 0)
+    exp = (inputs[0] + inputs[1]).astype(np.float32)
+    for r in range(2):
+        assert np.array_equal(recv[r].view(np.uint32), exp.view(np.uint32)), f"rank {r}"
+
+
+@pytest.mark.parametrize("n_ranks,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 0), (4, mg.I32, 3), (3, mg.F16, 4),
+                                           (2, mg.I8, 4), (5, mg.F64, 1)])
+def test_ring_device_memory_matches_fold_order(ring, oracle, n_ranks, dt, op):
+    from oracle.ring import ring_allreduce_expected
+    count = 300_001
+    inputs = mg.gen_inputs(dt, n_ranks, count, 31 * dt + op, special=True)
+    send = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+    recv = [torch.zeros_like(s) for s in send]
+    torch.cuda.synchronize()
+    with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 1 << 18) as comm:
+        comm.all_reduce([s.data_ptr() for s in send], [d.data_ptr() for d in recv], count, dt, op)
+    exp = ring_allreduce_expected(inputs, dt, op, 1 << 18)
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+def test_ring_host_memory_avg_three_ranks(ring, oracle):
+    from oracle.ring import ring_allreduce_expected
+    inputs = mg.gen_inputs(mg.BF16, 3, 70_003, 99, special=True)
+    recv = [np.zeros_like(x) for x in inputs]
+    with ring.RingComm(3, ring.HOST_MEMORY, 1 << 16) as comm:
+        comm.all_reduce([a.ctypes.data for a in inputs], [b.ctypes.data for b in recv], inputs[0].size, mg.BF16, 4)
+    exp = ring_allreduce_expected(inputs, mg.BF16, 4, 1 << 16)
+    for r in range(3):
+        assert np.array_equal(recv[r], exp[r])
