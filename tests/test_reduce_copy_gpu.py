@@ -263,3 +263,19 @@ def test_large_integer_sum_checksum_property(nexr, dev):
     torch.cuda.synchronize()
     assert int(o.sum()) == int(a.sum() + b.sum())
     assert torch.equal(o, a + b)
+
+
+def test_buffers_larger_than_4gib(nexr, dev):
+    # 64-bit offsets end to end: 4.5 Gi int8 elements per buffer (13.5 GiB in HBM), K=2 sum with
+    # wrap-around, checked on the device against torch's own uint8 add.
+    n = (9 << 30) // 2
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    a = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    b = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    o = torch.empty_like(a)
+    nexr.reduce_copy([a, b], [o], nexr.DevRedOp.Sum, datatype=nexr.DataType.Uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(o, a + b)
+    del a, b, o
+    torch.cuda.empty_cache()
