@@ -14,8 +14,8 @@
  *   - the caller owns every buffer; nothing is allocated or freed inside a hot call;
  *   - device calls are stream-ordered and asynchronous on the given HIP stream (NULL = the
  *     default stream of the current device); they never synchronise the host;
- *   - calls are safe concurrently on different devices / streams (no global mutable state apart
- *     from a per-device launch-geometry cache initialised once per device);
+ *   - calls are safe concurrently on different devices / streams (no global mutable state: tuning
+ *     knobs are read from the environment once; host staging resources are per thread and device);
  *   - errors are returned, never aborted on.
  */
 #ifndef NEXR_H_
@@ -111,9 +111,9 @@ typedef void* nexrStream_t; /* a hipStream_t; NULL = default stream */
  * fork's SKIP_COMP at reduce_kernel.h:432 removed; Min/Max compared at the signedness of
  * `datatype`). Rounding to T after every step; integer sum/prod wrap modulo 2^bits.
  *
- * Device pointers; any alignment; dsts may alias srcs[0] exactly (in-place). nElts == 0 is a
- * no-op. 1 <= nSrcs <= 8, 1 <= nDsts <= 8, 0 <= nPreOpSrcs <= nSrcs, preOpArgs may be NULL
- * when nPreOpSrcs == 0.
+ * Device pointers; any alignment; dsts may alias srcs[0] exactly (in-place). nElts == 0 or
+ * nDsts == 0 is a no-op (common_kernel.h:288-289). 1 <= nSrcs <= 8, 0 <= nDsts <= 8,
+ * 0 <= nPreOpSrcs <= nSrcs, preOpArgs may be NULL when nPreOpSrcs == 0.
  */
 NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
                                      size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
@@ -125,7 +125,11 @@ NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDs
  * transport's staging FIFOs, reference src/include/device.h:753-771): copies the K inputs
  * host->device, runs nexrReduceCopy, copies the M outputs device->host, and synchronises the
  * stream before returning. Device scratch is taken from a per-device cache grown on demand
- * (the only call that may allocate). Inputs may be pageable or pinned (pinned is faster).
+ * (the only call that may allocate). When every buffer is pinned host memory (hipHostMalloc /
+ * hipHostRegister / torch pin_memory) the kernel reads and writes it in place over PCIe (zero-copy,
+ * both directions concurrently; NEXR_HOST_ZERO_COPY=0 disables). Otherwise the call stages through
+ * device memory in chunks (NEXR_HOST_CHUNK_BYTES, default 8 MiB per buffer): chunk c is copied in
+ * and reduced while chunk c-1 is copied out on a second stream.
  */
 NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
                                          size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,

@@ -279,3 +279,35 @@ def test_buffers_larger_than_4gib(nexr, dev):
     assert torch.equal(o, a + b)
     del a, b, o
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("dt,n,op,name", [(mg.F32, 5_000_003, mg.SUM, "sum"), (mg.I8, 30_000_001, mg.MINMAX, "max"),
+                                          (mg.BF16, 9_000_017, mg.PROD, "prod")])
+def test_host_staged_pipeline_multi_chunk(nexr, oracle, dt, n, op, name, dev):
+    # several 8 MiB chunks with a ragged last one; copy-in of chunk c overlaps copy-out of c-1
+    srcs = mg.gen_inputs(dt, 3, n, 61 + dt, special=True)
+    arg = mg.minmax_arg(dt, True) if name == "max" else 0
+    exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
+    dsts = [np.zeros_like(srcs[0]) for _ in range(2)]
+    nexr.reduce_copy_ptrs([s.ctypes.data for s in srcs], [d.ctypes.data for d in dsts], n, dt, op, arg, host=True)
+    for d in dsts:
+        assert same(dt, d, exp)
+
+
+def test_host_zero_copy_pinned_buffers(nexr, oracle, dev):
+    # pinned (device-mapped) host buffers: the kernel reads/writes them in place over PCIe;
+    # interior pointers (offset into the allocation) and a pinned/pageable mix (-> staged) too.
+    n = 3_000_001
+    srcs = mg.gen_inputs(mg.F16, 4, n, 808, special=True)
+    exp = oracle.reduce_copy(srcs, 1, mg.F16, mg.SUM, threads=16)[0]
+    pin = [torch.empty(n * 2 + 64, dtype=torch.uint8).pin_memory() for _ in range(6)]
+    for p, s in zip(pin, srcs):
+        p[32:32 + n * 2].copy_(torch.from_numpy(s.view(np.uint8)))
+    sp = [p.data_ptr() + 32 for p in pin[:4]]
+    dp = [pin[4].data_ptr() + 32, pin[5].data_ptr() + 32]
+    nexr.reduce_copy_ptrs(sp, dp, n, mg.F16, mg.SUM, host=True)
+    for p in pin[4:]:
+        assert same(mg.F16, p[32:32 + n * 2].numpy().view(np.uint16), exp)
+    pageable = np.zeros_like(srcs[0])
+    nexr.reduce_copy_ptrs(sp, [pinned for pinned in dp[:1]] + [pageable.ctypes.data], n, mg.F16, mg.SUM, host=True)
+    assert same(mg.F16, pageable, exp)
