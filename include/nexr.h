@@ -153,6 +153,33 @@ NEXR_API nexrResult_t nexrHostToDevRedOp(nexrDevRedOpFull* opFull, int op, int d
 NEXR_API nexrResult_t nexrLaunchOneRank(void* dst, const void* src, size_t nElts, nexrDevRedOpFull redOp,
                                         int datatype, nexrStream_t stream);
 
+/* One LL-protocol FIFO line — identical layout to union ncclLLFifoLine (reference
+ * src/include/device.h:695-708): 8 data bytes split in two 32-bit halves, each followed by the
+ * step flag; a line is valid when flag1 == flag2 == the expected flag. */
+typedef struct {
+  uint32_t data1, flag1, data2, flag2;
+} nexrLLFifoLine;
+
+/*
+ * nexrReduceCopyLL — one step of the LL protocol's reduce-copy, LLGenericOp<RECV, SEND, SrcBuf,
+ * DstBuf> (reference src/device/prims_ll.h:218-283), with the step's FIFO slots resolved by the
+ * caller: recvLines[i] / sendLines[i] point at the peer's slot (recvPtr(i)/sendPtr(i), :38-41) and
+ * recvFlags[i] / sendFlags[i] are NCCL_LL_FLAG(step+1) (:42-43). Per 8-byte data line:
+ *   d = src (x redOpArg when srcIsInput and the op is PreMulSum: applyPreOp(redOp, ·))
+ *   d = nRecv ? (src ? op(peer0, d) : peer0) : d;  d = op(peer_i, d) for i >= 1   (peer FIRST)
+ *   d = postOp ? d / divisor : d                                                  (SumPostDiv)
+ *   sendLines[i] = {lo32(d), flag_i, hi32(d), flag_i};  dst = d  (valid elements only)
+ * Recv lines are polled until both flags match (system-scope loads), for at most timeoutUs
+ * (0 = 1 s); a line that never becomes valid sets *status = 1 (status: optional device/host-mapped
+ * word) and its outputs are left unwritten — the kernel never hangs. src/dst are any-aligned device
+ * pointers (nullable: at least one input and one output); line buffers must be 16-B aligned.
+ */
+NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
+                                       const uint32_t* recvFlags, void* dst, int nSend, void* const* sendLines,
+                                       const uint32_t* sendFlags, size_t nElts, int datatype, int devRedOp,
+                                       uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
+                                       nexrStream_t stream);
+
 /* Bytes per element of a datatype (reference ncclTypeSize), 0 if unknown. */
 NEXR_API size_t nexrTypeSize(int datatype);
 

@@ -77,7 +77,7 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
 
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
-               "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
+               "nexrReduceCopyLL", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
 
 
 class NexrError(RuntimeError):
@@ -118,6 +118,9 @@ def lib() -> ctypes.CDLL:
     L.nexrHostToDevRedOp.restype = i32
     L.nexrLaunchOneRank.argtypes = [vp, vp, sz, DevRedOpFull, i32, vp]
     L.nexrLaunchOneRank.restype = i32
+    L.nexrReduceCopyLL.argtypes = [vp, i32, i32, P(vp), P(ctypes.c_uint32), vp, i32, P(vp), P(ctypes.c_uint32), sz,
+                                   i32, i32, u64, i32, vp, ctypes.c_uint32, vp]
+    L.nexrReduceCopyLL.restype = i32
     L.nexrTypeSize.argtypes = [i32]
     L.nexrTypeSize.restype = sz
     L.nexrGetErrorString.argtypes = [i32]
@@ -184,6 +187,23 @@ def launch_one_rank(dst: int, src: int, n_elts: int, red_op: DevRedOpFull, datat
                                    ctypes.c_void_p(int(src)) if src else None, int(n_elts), red_op,
                                    int(datatype), ctypes.c_void_p(int(stream)) if stream else None),
            "nexrLaunchOneRank")
+
+
+def reduce_copy_ll(src: int, recv_lines: Sequence[int], recv_flags: Sequence[int], dst: int,
+                   send_lines: Sequence[int], send_flags: Sequence[int], n_elts: int, datatype: int,
+                   dev_red_op: int, red_op_arg: int = 0, src_is_input: bool = True, post_op: bool = False,
+                   status: int = 0, timeout_us: int = 0, stream: int = 0) -> None:
+    """One LL-protocol step (LLGenericOp, reference src/device/prims_ll.h:218-283) on device pointers."""
+    u32 = ctypes.c_uint32
+    rf = (u32 * max(1, len(recv_flags)))(*[int(f) & 0xFFFFFFFF for f in recv_flags])
+    sf = (u32 * max(1, len(send_flags)))(*[int(f) & 0xFFFFFFFF for f in send_flags])
+    rc = lib().nexrReduceCopyLL(ctypes.c_void_p(int(src)) if src else None, 1 if src_is_input else 0,
+                                len(recv_lines), _ptr_array(recv_lines), rf,
+                                ctypes.c_void_p(int(dst)) if dst else None, len(send_lines), _ptr_array(send_lines),
+                                sf, int(n_elts), int(datatype), int(dev_red_op), int(red_op_arg) & 0xFFFFFFFFFFFFFFFF,
+                                1 if post_op else 0, ctypes.c_void_p(int(status)) if status else None,
+                                int(timeout_us), ctypes.c_void_p(int(stream)) if stream else None)
+    _check(rc, "nexrReduceCopyLL")
 
 
 def version() -> int:

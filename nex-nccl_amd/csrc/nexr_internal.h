@@ -32,6 +32,22 @@ struct RCParams {
   int generic;
 };
 
+// Launch parameters of one LL-protocol step (nexr_ll.hip; reference src/device/prims_ll.h:218-283).
+struct LLParams {
+  const char* src;                  // user buffer (nullable)
+  const char* recv[NEXR_MAX_SRCS];  // peer LL lines of this step
+  uint32_t recvFlag[NEXR_MAX_SRCS];
+  char* dst;                        // user buffer (nullable)
+  char* send[NEXR_MAX_DSTS];
+  uint32_t sendFlag[NEXR_MAX_DSTS];
+  uint64_t nElts;
+  uint64_t redArg;
+  uint32_t* status;                 // set to 1 when a recv flag never arrived (nullable)
+  uint64_t timeoutTicks;            // s_memrealtime ticks (100 MHz) before giving up
+  int nRecv, nSend, srcIsInput, postOp;
+};
+hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s);
+
 // Launch geometry chosen by the host.
 struct Geometry {
   int grid;

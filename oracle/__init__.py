@@ -93,3 +93,45 @@ def host_to_dev_red_op(op: int, datatype: int, n_ranks: int):
 
 def onerank_reference_coverage(n_elts: int, datatype: int) -> int:
     return int(lib().oracle_onerank_reference_coverage(int(n_elts), int(datatype)))
+
+
+def reduce_copy_ll(src, src_is_input, recv_lines, recv_flags, with_dst, n_send, send_flags, n_elts, datatype,
+                   dev_red_op, red_op_arg=0, post_op=False):
+    """One LL step on numpy buffers (lines: uint8 arrays of 16 B per line). Returns (rc, dst, sends)."""
+    L = lib()
+    if not hasattr(L, "_ll_ready"):
+        vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+        P = ctypes.POINTER
+        L.oracle_reduce_copy_ll.argtypes = [vp, ctypes.c_int, ctypes.c_int, P(vp), P(u32), vp, ctypes.c_int, P(vp),
+                                            P(u32), ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                            ctypes.c_int]
+        L.oracle_reduce_copy_ll.restype = ctypes.c_int
+        L._ll_ready = True
+    esz = L.oracle_type_size(int(datatype))
+    n_lines = (n_elts * esz + 7) // 8
+    dst = np.zeros(n_elts * esz, dtype=np.uint8) if with_dst else None
+    sends = [np.zeros(n_lines * 16, dtype=np.uint8) for _ in range(n_send)]
+    rl = (ctypes.c_void_p * max(1, len(recv_lines)))(*[x.ctypes.data for x in recv_lines])
+    rf = (ctypes.c_uint32 * max(1, len(recv_flags)))(*recv_flags)
+    sl = (ctypes.c_void_p * max(1, n_send))(*[x.ctypes.data for x in sends])
+    sf = (ctypes.c_uint32 * max(1, len(send_flags)))(*send_flags)
+    rc = L.oracle_reduce_copy_ll(src.ctypes.data if src is not None else None, 1 if src_is_input else 0,
+                                 len(recv_lines), rl, rf, dst.ctypes.data if dst is not None else None, n_send, sl, sf,
+                                 int(n_elts), int(datatype), int(dev_red_op), int(red_op_arg) & 0xFFFFFFFFFFFFFFFF,
+                                 1 if post_op else 0)
+    return rc, dst, sends
+
+
+def make_ll_lines(data: np.ndarray, flag: int) -> np.ndarray:
+    """Encode raw data bytes as LL lines {data1, flag, data2, flag} (ncclLLFifoLine), zero-padded."""
+    raw = np.ascontiguousarray(data).view(np.uint8)
+    n_lines = (raw.size + 7) // 8
+    padded = np.zeros(n_lines * 8, dtype=np.uint8)
+    padded[:raw.size] = raw
+    words = padded.view(np.uint32).reshape(n_lines, 2)
+    lines = np.empty((n_lines, 4), dtype=np.uint32)
+    lines[:, 0] = words[:, 0]
+    lines[:, 1] = flag
+    lines[:, 2] = words[:, 1]
+    lines[:, 3] = flag
+    return lines.reshape(-1).view(np.uint8)

@@ -315,6 +315,92 @@ int oracle_reduce_copy_mt(int nSrcs, const void* const* srcs, int nDsts, void* c
   return R_OK;
 }
 
+/* ---- LL protocol step (reference src/device/prims_ll.h:218-283) ------------------------------ */
+/* One element through one reduce step with the PEER as the first operand: out = op(c, v). */
+static void elem_reduce(int dt, const Fn* fn, const uint8_t* c, const uint8_t* v, uint8_t* out) {
+  switch (dt) {
+    case DT_I8: case DT_U8: { uint8_t a = *c, b = *v, r = dt == DT_I8 ? red_uint8_t_1(fn, a, b) : red_uint8_t_0(fn, a, b); *out = r; break; }
+    case DT_I32: case DT_U32: { uint32_t a, b, r; memcpy(&a, c, 4); memcpy(&b, v, 4);
+      r = dt == DT_I32 ? red_uint32_t_1(fn, a, b) : red_uint32_t_0(fn, a, b); memcpy(out, &r, 4); break; }
+    case DT_I64: case DT_U64: { uint64_t a, b, r; memcpy(&a, c, 8); memcpy(&b, v, 8);
+      r = dt == DT_I64 ? red_uint64_t_1(fn, a, b) : red_uint64_t_0(fn, a, b); memcpy(out, &r, 8); break; }
+    case DT_F32: { float a, b, r; memcpy(&a, c, 4); memcpy(&b, v, 4); r = red_f32(fn, a, b); memcpy(out, &r, 4); break; }
+    case DT_F64: { double a, b, r; memcpy(&a, c, 8); memcpy(&b, v, 8); r = red_f64(fn, a, b); memcpy(out, &r, 8); break; }
+    case DT_F16: { uint16_t a, b, r; memcpy(&a, c, 2); memcpy(&b, v, 2); r = red_f16(fn, a, b); memcpy(out, &r, 2); break; }
+    case DT_BF16: { uint16_t a, b, r; memcpy(&a, c, 2); memcpy(&b, v, 2); r = red_bf16(fn, a, b); memcpy(out, &r, 2); break; }
+  }
+}
+/* applyPreOp(FuncPreMulSum(raw), x) */
+static void elem_premul(int dt, uint64_t raw, uint8_t* x) {
+  switch (dt) {
+    case DT_I8: case DT_U8: *x = (uint8_t)(*x * (uint8_t)raw); break;
+    case DT_I32: case DT_U32: { uint32_t a; memcpy(&a, x, 4); a = a * (uint32_t)raw; memcpy(x, &a, 4); break; }
+    case DT_I64: case DT_U64: { uint64_t a; memcpy(&a, x, 8); a = a * raw; memcpy(x, &a, 8); break; }
+    case DT_F32: { float a; memcpy(&a, x, 4); a = a * u2f((uint32_t)raw); memcpy(x, &a, 4); break; }
+    case DT_F64: { double a; memcpy(&a, x, 8); a = a * u2d(raw); memcpy(x, &a, 8); break; }
+    case DT_F16: { uint16_t a; memcpy(&a, x, 2);
+      a = oracle_float_to_half(oracle_half_to_float(a) * oracle_half_to_float((uint16_t)raw)); memcpy(x, &a, 2); break; }
+    case DT_BF16: { uint16_t a; memcpy(&a, x, 2);
+      a = oracle_float_to_bf16(oracle_bf16_to_float(a) * oracle_bf16_to_float((uint16_t)raw)); memcpy(x, &a, 2); break; }
+  }
+}
+static void elem_postdiv(int dt, const Fn* fn, uint8_t* x) {
+  switch (dt) {
+    case DT_I8: case DT_U8: *x = div_u8(fn, *x); break;
+    case DT_I32: case DT_U32: { uint32_t a; memcpy(&a, x, 4); a = div_u32(fn, a); memcpy(x, &a, 4); break; }
+    case DT_I64: case DT_U64: { uint64_t a; memcpy(&a, x, 8); a = div_u64(fn, a); memcpy(x, &a, 8); break; }
+  }
+}
+
+/* Lines are 16 bytes {data1, flag1, data2, flag2} (union ncclLLFifoLine). Returns 0, 4 (bad
+ * arguments) or 3 when a recv line does not carry the expected flags (the device would wait). */
+int oracle_reduce_copy_ll(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
+                          const uint32_t* recvFlags, void* dst, int nSend, void* const* sendLines,
+                          const uint32_t* sendFlags, size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                          int postOp) {
+  int r = check(1, 0, datatype, devRedOp, redOpArg, 0, NULL);
+  if (r != R_OK) return r;
+  if (nRecv < 0 || nRecv > 8 || nSend < 0 || nSend > 8 || (!src && !nRecv) || (!dst && !nSend)) return R_INVALID;
+  Fn fn;
+  make_fn(&fn, devRedOp, redOpArg);
+  const size_t esz = oracle_type_size(datatype);
+  const size_t epl = 8 / esz;
+  const size_t nLines = (nElts * esz + 7) / 8;
+  for (size_t l = 0; l < nLines; l++) {
+    size_t eltN = nElts - l * epl < epl ? nElts - l * epl : epl;
+    uint8_t d[8] = {0};
+    if (src) {
+      memcpy(d, (const uint8_t*)src + l * 8, eltN * esz);
+      if (devRedOp == OP_PREMULSUM && srcIsInput)
+        for (size_t e = 0; e < epl; e++) elem_premul(datatype, redOpArg, d + e * esz);
+    }
+    for (int i = 0; i < nRecv; i++) {
+      const uint8_t* line = (const uint8_t*)recvLines[i] + l * 16;
+      uint32_t f1, f2;
+      memcpy(&f1, line + 4, 4);
+      memcpy(&f2, line + 12, 4);
+      if (f1 != recvFlags[i] || f2 != recvFlags[i]) return 3;
+      uint8_t peer[8];
+      memcpy(peer, line, 4);
+      memcpy(peer + 4, line + 8, 4);
+      if (i == 0 && !src) memcpy(d, peer, 8);
+      else
+        for (size_t e = 0; e < epl; e++) elem_reduce(datatype, &fn, peer + e * esz, d + e * esz, d + e * esz);
+    }
+    if (devRedOp == OP_SUMPOSTDIV && postOp)
+      for (size_t e = 0; e < epl; e++) elem_postdiv(datatype, &fn, d + e * esz);
+    for (int i = 0; i < nSend; i++) {
+      uint8_t* line = (uint8_t*)sendLines[i] + l * 16;
+      memcpy(line, d, 4);
+      memcpy(line + 4, &sendFlags[i], 4);
+      memcpy(line + 8, d + 4, 4);
+      memcpy(line + 12, &sendFlags[i], 4);
+    }
+    if (dst) memcpy((uint8_t*)dst + l * 8, d, eltN * esz);
+  }
+  return R_OK;
+}
+
 /* hostToDevRedOp restated (reference src/enqueue.cc:2185-2278), built-in ops only.
  * out[0] = devRedOp, out[1] = scalarArg. Returns 0 or 4. */
 int oracle_host_to_dev_redop(int op, int datatype, int nRanks, uint64_t* out) {
