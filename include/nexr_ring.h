@@ -10,6 +10,9 @@
  *   - the FIFO credit protocol of waitPeer/postPeer (prims_simple.h:111-188): NCCL_STEPS = 8 slots of
  *     buffBytes/8 per connection, head/tail step counters, StepPerSlice = 2, SlicePerChunk = 2
  *     (src/include/collectives.h:17-18),
+ *   - or, with protocol = LL, LLGenericOp's one-step-per-call credits and line flags
+ *     NCCL_LL_FLAG(step+1) (src/device/prims_ll.h:55-93, :218-283; chunk = stepSize/2,
+ *     src/enqueue.cc:1997),
  *   - the host chunking for ring SIMPLE (src/enqueue.cc:1993-1996: chunkSize = stepSize * 4),
  *   - ncclLaunchOneRank for nRanks == 1 (src/device/onerank.cc:48-83),
  *   - op encoding through nexrHostToDevRedOp (src/enqueue.cc:2185-2278).
@@ -31,14 +34,27 @@ typedef nexrResult_t (*nexrReduceCopyFn)(int nSrcs, const void* const* srcs, int
                                          int nPreOpSrcs, const uint64_t* preOpArgs, int postOp,
                                          nexrStream_t stream);
 
+/* Same signature as nexrReduceCopyLL. */
+typedef nexrResult_t (*nexrReduceCopyLLFn)(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
+                                           const uint32_t* recvFlags, void* dst, int nSend, void* const* sendLines,
+                                           const uint32_t* sendFlags, size_t nElts, int datatype, int devRedOp,
+                                           uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
+                                           nexrStream_t stream);
+
 typedef enum { nexrRingHostMemory = 0, nexrRingDeviceMemory = 1 } nexrRingMemMode_t;
+/* The two protocols the emulated ring restates (the reference's NCCL_PROTO_SIMPLE / NCCL_PROTO_LL).
+ * Numbered so that a zero-initialised config selects SIMPLE. */
+typedef enum { nexrRingProtoSimple = 0, nexrRingProtoLL = 1 } nexrRingProto_t;
 
 typedef struct {
   int nRanks;          /* emulated ranks (threads), >= 1 */
-  size_t buffBytes;    /* per-connection SIMPLE buffer (NCCL_BUFFSIZE); 0 = 4 MiB default */
+  size_t buffBytes;    /* per-connection buffer (NCCL_BUFFSIZE); 0 = the protocol default: 4 MiB
+                          SIMPLE, 512 KiB LL (src/init.cc:618-631) */
   int memMode;         /* nexrRingMemMode_t: where user buffers and FIFOs live */
-  nexrReduceCopyFn fn; /* NULL = nexrReduceCopyHost (host mode) / nexrReduceCopy (device mode) */
+  nexrReduceCopyFn fn; /* SIMPLE: NULL = nexrReduceCopyHost (host) / nexrReduceCopy (device) */
   int timeoutMs;       /* spin-wait bound per FIFO wait; 0 = 60000 */
+  int protocol;        /* nexrRingProto_t (0 = SIMPLE) */
+  nexrReduceCopyLLFn llFn; /* LL: NULL = nexrReduceCopyLL (device memory mode only) */
 } nexrRingConfig;
 
 typedef struct nexrRingComm* nexrRingComm_t;

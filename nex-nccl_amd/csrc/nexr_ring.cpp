@@ -22,6 +22,7 @@ constexpr int kSliceSteps = kSteps / 4;                  // ALLREDUCE_SLICESTEPS
 constexpr int kChunkSteps = kSteps / 2;                  // ALLREDUCE_CHUNKSTEPS (collectives.h:18)
 constexpr int kSlicePerChunk = kChunkSteps / kSliceSteps;
 constexpr size_t kDefaultBuffBytes = 4u << 20;           // NCCL_BUFFSIZE default (init.cc:620-634)
+constexpr size_t kDefaultLLBuffBytes = 8 * 512 * kSteps * 16;  // DEFAULT_LL_BUFFSIZE (init.cc:618)
 
 // One directed connection prev -> r. The FIFO belongs to the receiver (the sender writes into it,
 // like a P2P/SHM transport's recv buffer, src/include/device.h:753-771).
@@ -44,6 +45,9 @@ struct nexrRingComm {
   std::vector<uint64_t> sendStep;    // per rank: next step to produce into conns[(r+1)%n]
   std::vector<int> devices;
   std::vector<hipStream_t> streams;
+  std::vector<uint32_t*> status;     // LL: per-rank pinned status word the kernel reports timeouts in
+  bool ll = false;
+  bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
   bool broken = false;
 };
 
@@ -73,6 +77,8 @@ struct Prims {
   int datatype, devOp;
   uint64_t redOpArgs[1];
   nexrReduceCopyFn fn;
+  nexrReduceCopyLLFn llFn;
+  uint32_t* status;
   hipStream_t stream;
   bool device;
 
@@ -154,20 +160,64 @@ struct Prims {
     }
     return true;
   }
-  bool directSend(int64_t inpIx, int64_t n) { return genericOp(false, true, true, false, inpIx, -1, n, false); }
-  bool directRecvReduceDirectSend(int64_t inpIx, int64_t n) { return genericOp(true, true, true, false, inpIx, -1, n, false); }
-  bool directRecvReduceCopyDirectSend(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
-    return genericOp(true, true, true, true, inpIx, outIx, n, postOp);
+  // LLGenericOp<RECV, SEND, SrcBuf, DstBuf> (prims_ll.h:218-283): one FIFO step per call. The
+  // sender waits for a credit (waitSend :55-75); the receiver's data readiness is the line flags
+  // NCCL_LL_FLAG(step+1) (:42-43). The host additionally waits for the sender's step so that the
+  // kernel's flag poll succeeds at once: two emulated ranks may share one GPU, and a kernel spinning
+  // on a producer that cannot be scheduled beside it must never be launched.
+  bool genericOpLL(bool Recv, bool Send, bool Src, bool Dst, int64_t srcIx, int64_t dstIx, int64_t nelem,
+                   bool postOp) {
+    nelem = nelem < 0 ? 0 : nelem;
+    uint64_t& rs = c->recvStep[rank];
+    uint64_t& ss = c->sendStep[rank];
+    if (Send && ss + 1 > (uint64_t)kSteps && !waitAtLeast(sendConn->head, ss + 1 - kSteps)) return false;
+    if (Recv && !waitAtLeast(recvConn->tail, rs + 1)) return false;
+    if (nelem > 0) {
+      const void* recvLines[1] = {recvConn->fifo + (rs % kSteps) * c->stepBytes};
+      void* sendLines[1] = {sendConn->fifo + (ss % kSteps) * c->stepBytes};
+      const uint32_t recvFlag[1] = {(uint32_t)(rs + 1)};  // NCCL_LL_FLAG(recvStep+1)
+      const uint32_t sendFlag[1] = {(uint32_t)(ss + 1)};
+      if (status) *status = 0;
+      nexrResult_t r = llFn(Src ? userInput + srcIx * esz : nullptr, Src ? 1 : 0, Recv ? 1 : 0, recvLines, recvFlag,
+                            Dst ? userOutput + dstIx * esz : nullptr, Send ? 1 : 0, sendLines, sendFlag,
+                            (size_t)nelem, datatype, devOp, redOpArgs[0], postOp ? 1 : 0, status,
+                            (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u), (nexrStream_t)stream);
+      if (r == nexrSuccess && device && hipStreamSynchronize(stream) != hipSuccess) r = nexrUnhandledCudaError;
+      if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
+      if (r != nexrSuccess) {
+        sh->fail(r);
+        return false;
+      }
+    }
+    if (Recv) {  // postRecv (:80-83)
+      rs += 1;
+      recvConn->head.store(rs, std::memory_order_release);
+    }
+    if (Send) {  // incSend (:85-93); the flag-wrap cleanup at NCCL_LL_CLEAN_MASK needs ~2^31 steps
+      ss += 1;
+      sendConn->tail.store(ss, std::memory_order_release);
+    }
+    return true;
   }
-  bool directRecvCopyDirectSend(int64_t outIx, int64_t n) { return genericOp(true, true, false, true, -1, outIx, n, false); }
-  bool directRecv(int64_t outIx, int64_t n) { return genericOp(true, false, false, true, -1, outIx, n, false); }
+  bool op(bool Recv, bool Send, bool Src, bool Dst, int64_t srcIx, int64_t dstIx, int64_t n, bool postOp) {
+    return c->ll ? genericOpLL(Recv, Send, Src, Dst, srcIx, dstIx, n, postOp)
+                 : genericOp(Recv, Send, Src, Dst, srcIx, dstIx, n, postOp);
+  }
+  bool directSend(int64_t inpIx, int64_t n) { return op(false, true, true, false, inpIx, -1, n, false); }
+  bool directRecvReduceDirectSend(int64_t inpIx, int64_t n) { return op(true, true, true, false, inpIx, -1, n, false); }
+  bool directRecvReduceCopyDirectSend(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
+    return op(true, true, true, true, inpIx, outIx, n, postOp);
+  }
+  bool directRecvCopyDirectSend(int64_t outIx, int64_t n) { return op(true, true, false, true, -1, outIx, n, false); }
+  bool directRecv(int64_t outIx, int64_t n) { return op(true, false, false, true, -1, outIx, n, false); }
 };
 
 // runRing<T, RedOp, ProtoSimple> (all_reduce.h:12-84) for one rank, 1 channel (gridOffset 0,
 // channelCount = count, chunkCount = chunkSize / sizeof(T): enqueue.cc:1993-1996, :655-678).
 void runRing(Prims& p, int nranks, int64_t count) {
   const int ringIx = p.rank;
-  int64_t chunkCount = (int64_t)(p.c->stepBytes * kChunkSteps / p.esz);
+  // SIMPLE: chunkSize = stepSize * chunkSteps; LL: stepSize / 2 (enqueue.cc:1993-1997)
+  int64_t chunkCount = p.c->ll ? (int64_t)(p.c->stepBytes / 2 / p.esz) : (int64_t)(p.c->stepBytes * kChunkSteps / p.esz);
   const int64_t loopCount = nranks * chunkCount;
   auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
   for (int64_t elemOffset = 0; elemOffset < count; elemOffset += loopCount) {
@@ -205,6 +255,13 @@ nexrResult_t defaultHostFn(int nSrcs, const void* const* srcs, int nDsts, void* 
                            int op, uint64_t arg, int nPre, const uint64_t* pre, int post, nexrStream_t s) {
   return nexrReduceCopyHost(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
 }
+nexrResult_t defaultLLFn(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
+                         const uint32_t* recvFlags, void* dst, int nSend, void* const* sendLines,
+                         const uint32_t* sendFlags, size_t n, int dt, int op, uint64_t arg, int post, uint32_t* status,
+                         uint32_t timeoutUs, nexrStream_t s) {
+  return nexrReduceCopyLL(src, srcIsInput, nRecv, recvLines, recvFlags, dst, nSend, sendLines, sendFlags, n, dt, op,
+                          arg, post, status, timeoutUs, s);
+}
 nexrResult_t defaultDeviceFn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t n, int dt,
                              int op, uint64_t arg, int nPre, const uint64_t* pre, int post, nexrStream_t s) {
   return nexrReduceCopy(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
@@ -217,22 +274,31 @@ extern "C" {
 NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConfig* cfg) {
   if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024) return nexrInvalidArgument;
   if (cfg->memMode != nexrRingHostMemory && cfg->memMode != nexrRingDeviceMemory) return nexrInvalidArgument;
+  if (cfg->protocol != nexrRingProtoSimple && cfg->protocol != nexrRingProtoLL) return nexrInvalidArgument;
+  // The LL kernel polls live FIFO lines: it needs device-visible lines, i.e. device memory, unless
+  // the caller supplies its own LL implementation (e.g. a CPU checker).
+  if (cfg->protocol == nexrRingProtoLL && cfg->memMode == nexrRingHostMemory && !cfg->llFn) return nexrInvalidUsage;
   auto* c = new nexrRingComm();
   c->cfg = *cfg;
-  if (c->cfg.buffBytes == 0) c->cfg.buffBytes = kDefaultBuffBytes;
+  c->ll = cfg->protocol == nexrRingProtoLL;
+  if (c->cfg.buffBytes == 0) c->cfg.buffBytes = c->ll ? kDefaultLLBuffBytes : kDefaultBuffBytes;
   if (c->cfg.buffBytes % (kSteps * 16) != 0) {
     delete c;
     return nexrInvalidArgument;
   }
   if (!c->cfg.fn) c->cfg.fn = cfg->memMode == nexrRingDeviceMemory ? defaultDeviceFn : defaultHostFn;
+  if (!c->cfg.llFn) c->cfg.llFn = defaultLLFn;
   c->stepBytes = c->cfg.buffBytes / kSteps;
   const int n = cfg->nRanks;
   c->recvStep.assign(n, 0);
   c->sendStep.assign(n, 0);
   c->devices.assign(n, 0);
   c->streams.assign(n, nullptr);
+  c->status.assign(n, nullptr);
   int nDev = 0;
-  if (cfg->memMode == nexrRingDeviceMemory || !cfg->fn) {
+  const bool needHip = cfg->memMode == nexrRingDeviceMemory || (!c->ll && !cfg->fn) || (c->ll && !cfg->llFn);
+  c->pinnedStatus = needHip;
+  if (needHip) {
     if (hipGetDeviceCount(&nDev) != hipSuccess || nDev < 1) {
       delete c;
       return nexrUnhandledCudaError;
@@ -245,6 +311,19 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
       if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams[r]) != hipSuccess) {
         nexrRingCommDestroy(c);
         return nexrUnhandledCudaError;
+      }
+    }
+    if (c->ll && needHip) {  // pinned, device-mapped status word for the LL kernel's timeout report
+      if (hipHostMalloc((void**)&c->status[r], sizeof(uint32_t), hipHostMallocMapped) != hipSuccess) {
+        nexrRingCommDestroy(c);
+        return nexrUnhandledCudaError;
+      }
+      *c->status[r] = 0;
+    } else if (c->ll) {  // CPU-side LL implementation: an ordinary host word
+      c->status[r] = (uint32_t*)calloc(1, sizeof(uint32_t));
+      if (!c->status[r]) {
+        nexrRingCommDestroy(c);
+        return nexrSystemError;
       }
     }
     if (cfg->memMode == nexrRingDeviceMemory) {
@@ -332,6 +411,8 @@ NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sen
       p.devOp = red.op;
       p.redOpArgs[0] = red.scalarArg;
       p.fn = c->cfg.fn;
+      p.llFn = c->cfg.llFn;
+      p.status = c->status[rank];
       p.stream = c->streams[rank];
       p.device = device;
       runRing(p, n, (int64_t)count);
@@ -359,6 +440,11 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
     }
     delete k;
   }
+  for (size_t r = 0; r < c->status.size(); r++)
+    if (c->status[r]) {
+      if (c->pinnedStatus) (void)hipHostFree(c->status[r]);
+      else free(c->status[r]);
+    }
   for (size_t r = 0; r < c->streams.size(); r++)
     if (c->streams[r]) {
       (void)hipSetDevice(c->devices[r]);

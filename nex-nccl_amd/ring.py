@@ -18,6 +18,8 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingCommDest
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
+PROTO_SIMPLE = 0
+PROTO_LL = 1
 
 REDUCE_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
@@ -27,7 +29,8 @@ REDUCE_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(cty
 
 class RingConfig(ctypes.Structure):
     _fields_ = [("nRanks", ctypes.c_int), ("buffBytes", ctypes.c_size_t), ("memMode", ctypes.c_int),
-                ("fn", ctypes.c_void_p), ("timeoutMs", ctypes.c_int)]
+                ("fn", ctypes.c_void_p), ("timeoutMs", ctypes.c_int), ("protocol", ctypes.c_int),
+                ("llFn", ctypes.c_void_p)]
 
 
 _ring = None
@@ -55,8 +58,10 @@ class RingComm:
     """N emulated ranks (host threads) joined in one ring; `all_reduce` runs ncclAllReduce on all."""
 
     def __init__(self, n_ranks: int, mem_mode: int = HOST_MEMORY, buff_bytes: int = 0,
-                 fn_address: Optional[int] = None, timeout_ms: int = 0):
-        cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms)
+                 fn_address: Optional[int] = None, timeout_ms: int = 0, protocol: int = PROTO_SIMPLE,
+                 ll_fn_address: Optional[int] = None):
+        cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms, protocol,
+                         ll_fn_address or None)
         h = ctypes.c_void_p()
         _check(ring_lib().nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
         self._h = h

@@ -64,3 +64,41 @@ def ring_allreduce_expected(inputs, datatype: int, op: int, buff_bytes: int = 4 
                 acc = reduce_copy([inputs[r][sl], acc], 1, datatype, dev_op, arg, [arg], post)[0]
             out[sl] = acc
     return [out.copy() for _ in range(n)]
+
+
+def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int = 8 * 512 * 8 * 16):
+    """The LL-protocol ring: same runRing schedule (chunk = stepBytes/2, src/enqueue.cc:1997), but
+    every step folds with the received PEER partial as the first operand (prims_ll.h:251-258)."""
+    from . import make_ll_lines, reduce_copy_ll
+    n = len(inputs)
+    enc = host_to_dev_red_op(op, datatype, n)
+    if enc is None:
+        raise ValueError("op not encodable")
+    dev_op, arg = enc
+    count = inputs[0].size
+    esz = inputs[0].itemsize
+    if count == 0 or n == 1:
+        return ring_allreduce_expected(inputs, datatype, op)
+    out = np.empty_like(inputs[0])
+    chunk = (buff_bytes // 8) // 2 // esz
+    loop = n * chunk
+    for elem_off in range(0, count, loop):
+        rem = count - elem_off
+        if rem < loop:
+            chunk = _align_up(_div_up(rem, n), 16 // esz)
+        for c in range(n):
+            lo = elem_off + c * chunk
+            hi = min(lo + chunk, count)
+            if hi <= lo:
+                continue
+            m = hi - lo
+            r = (c + 1) % n
+            rc, _, sends = reduce_copy_ll(inputs[r][lo:hi], True, [], [], False, 1, [1], m, datatype, dev_op, arg)
+            for k in range(2, n + 1):
+                r = (c + k) % n
+                post = k == n
+                rc, dst, sends = reduce_copy_ll(inputs[r][lo:hi], True, [sends[0]], [1], post, 1, [1], m, datatype,
+                                                dev_op, arg, post)
+                assert rc == 0
+            out[lo:hi] = dst.view(out.dtype)
+    return [out.copy() for _ in range(n)]

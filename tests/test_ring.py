@@ -104,3 +104,29 @@ def test_ring_rejects_bad_arguments(ring, oracle_fn, nexr):
             comm.all_reduce([a.ctypes.data] * 2, [a.ctypes.data] * 2, 16, 10, 0)  # fp8
         with pytest.raises(nexr.NexrError):
             comm.all_reduce([a.ctypes.data] * 2, [a.ctypes.data] * 2, 16, mg.F32, 9)  # user op
+
+
+@pytest.fixture(scope="module")
+def oracle_ll_fn(oracle):
+    return ctypes.cast(oracle.lib().oracle_reduce_copy_ll_fn, ctypes.c_void_p).value
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3, 5])
+@pytest.mark.parametrize("dt,op,special", [(mg.F32, 0, False), (mg.BF16, 0, True), (mg.I32, 3, True),
+                                           (mg.F16, 4, True), (mg.I8, 4, True), (mg.F64, 2, True)])
+def test_ll_ring_matches_peer_first_fold_oracle(ring, oracle, oracle_ll_fn, n_ranks, dt, op, special):
+    from oracle.ring import ring_allreduce_expected_ll
+    buff = 8 * 1024 * 16  # 16 KiB LL steps: many loops and credit stalls
+    count = 20_000 + 3 * n_ranks
+    inputs = mg.gen_inputs(dt, n_ranks, count, 0xB00 + dt * 13 + op, special)
+    recv = [np.zeros_like(x) for x in inputs]
+    with ring.RingComm(n_ranks, ring.HOST_MEMORY, buff, None, 20000, ring.PROTO_LL, oracle_ll_fn) as comm:
+        comm.all_reduce([a.ctypes.data for a in inputs], [b.ctypes.data for b in recv], count, dt, op)
+    exp = ring_allreduce_expected_ll(inputs, dt, op, buff)
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, recv[r]) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+def test_ll_ring_needs_device_memory_or_a_custom_step(ring, nexr):
+    with pytest.raises(nexr.NexrError):
+        ring.RingComm(2, ring.HOST_MEMORY, 0, None, 0, ring.PROTO_LL, None)

@@ -54,3 +54,20 @@ def test_ring_host_memory_avg_three_ranks(ring, oracle):
     exp = ring_allreduce_expected(inputs, mg.BF16, 4, 1 << 16)
     for r in range(3):
         assert np.array_equal(recv[r], exp[r])
+
+
+@pytest.mark.parametrize("n_ranks,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 0), (4, mg.I8, 2), (3, mg.F16, 4)])
+def test_ll_ring_device_memory(ring, oracle, n_ranks, dt, op):
+    # the LL protocol end to end: line flags NCCL_LL_FLAG(step+1) produced by one rank's kernel and
+    # checked by the next rank's kernel, peer-first folds, 8-step credits
+    from oracle.ring import ring_allreduce_expected_ll
+    count = (1 << 20) + 5
+    inputs = mg.gen_inputs(dt, n_ranks, count, 57 * dt + op, special=True)
+    send = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+    recv = [torch.zeros_like(s) for s in send]
+    torch.cuda.synchronize()
+    with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 0, None, 20000, ring.PROTO_LL) as comm:
+        comm.all_reduce([s.data_ptr() for s in send], [d.data_ptr() for d in recv], count, dt, op)
+    exp = ring_allreduce_expected_ll(inputs, dt, op)
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
