@@ -180,6 +180,23 @@ NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRec
                                        uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
                                        nexrStream_t stream);
 
+/*
+ * nexrReduceCopyLL128 — one step of the LL128 protocol's reduce-copy, GenericOp +
+ * recvReduceSendCopy (reference src/device/prims_ll128.h:184-331), the step's slots resolved by the
+ * caller (recvPtr(i)/sendPtr(i), flags = step+1 as 64-bit words, :45-50). Wire format: 2 KiB slices
+ * of sixteen 128-B lines carrying 1920 data bytes; word 15 of every line is the flag; user 16-B
+ * chunk ix = g*32 - 4*(g/2) + w - (g%2)*(w/8) of a slice sits at wire words 64g + 2w (+1) for
+ * w % 8 != 7, and the w % 8 == 7 chunks are split over words 64g + 2w of g and g+1 (loadRegsBegin/
+ * loadRegsFinish/storeRegs :86-174) — byte-identical to the reference's warp-32 layout. Arithmetic,
+ * peer-first operand order, status/timeout and pointer rules as nexrReduceCopyLL; wire buffers must
+ * be 16-B aligned and hold ceil(nElts*size/1920) slices.
+ */
+NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
+                                          const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
+                                          const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
+                                          uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
+                                          nexrStream_t stream);
+
 /* Bytes per element of a datatype (reference ncclTypeSize), 0 if unknown. */
 NEXR_API size_t nexrTypeSize(int datatype);
 

@@ -77,7 +77,7 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
 
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
-               "nexrReduceCopyLL", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
+               "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
 
 
 class NexrError(RuntimeError):
@@ -121,6 +121,9 @@ def lib() -> ctypes.CDLL:
     L.nexrReduceCopyLL.argtypes = [vp, i32, i32, P(vp), P(ctypes.c_uint32), vp, i32, P(vp), P(ctypes.c_uint32), sz,
                                    i32, i32, u64, i32, vp, ctypes.c_uint32, vp]
     L.nexrReduceCopyLL.restype = i32
+    L.nexrReduceCopyLL128.argtypes = [vp, i32, i32, P(vp), P(u64), vp, i32, P(vp), P(u64), sz,
+                                      i32, i32, u64, i32, vp, ctypes.c_uint32, vp]
+    L.nexrReduceCopyLL128.restype = i32
     L.nexrTypeSize.argtypes = [i32]
     L.nexrTypeSize.restype = sz
     L.nexrGetErrorString.argtypes = [i32]
@@ -204,6 +207,23 @@ def reduce_copy_ll(src: int, recv_lines: Sequence[int], recv_flags: Sequence[int
                                 1 if post_op else 0, ctypes.c_void_p(int(status)) if status else None,
                                 int(timeout_us), ctypes.c_void_p(int(stream)) if stream else None)
     _check(rc, "nexrReduceCopyLL")
+
+
+def reduce_copy_ll128(src: int, recv_wire: Sequence[int], recv_flags: Sequence[int], dst: int,
+                      send_wire: Sequence[int], send_flags: Sequence[int], n_elts: int, datatype: int,
+                      dev_red_op: int, red_op_arg: int = 0, src_is_input: bool = True, post_op: bool = False,
+                      status: int = 0, timeout_us: int = 0, stream: int = 0) -> None:
+    """One LL128-protocol step (prims_ll128.h:184-331) on device pointers."""
+    rf = _u64_array(list(recv_flags)) if recv_flags else None
+    sf = _u64_array(list(send_flags)) if send_flags else None
+    rc = lib().nexrReduceCopyLL128(ctypes.c_void_p(int(src)) if src else None, 1 if src_is_input else 0,
+                                   len(recv_wire), _ptr_array(recv_wire), rf,
+                                   ctypes.c_void_p(int(dst)) if dst else None, len(send_wire), _ptr_array(send_wire),
+                                   sf, int(n_elts), int(datatype), int(dev_red_op),
+                                   int(red_op_arg) & 0xFFFFFFFFFFFFFFFF, 1 if post_op else 0,
+                                   ctypes.c_void_p(int(status)) if status else None, int(timeout_us),
+                                   ctypes.c_void_p(int(stream)) if stream else None)
+    _check(rc, "nexrReduceCopyLL128")
 
 
 def version() -> int:

@@ -442,6 +442,53 @@ NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRec
   return nexrSuccess;
 }
 
+NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
+                                          const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
+                                          const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
+                                          uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
+                                          nexrStream_t stream) {
+  if (nRecv < 0 || nRecv > NEXR_MAX_SRCS || nSend < 0 || nSend > NEXR_MAX_DSTS) return nexrInvalidArgument;
+  if ((!src && nRecv == 0) || (!dst && nSend == 0)) return nexrInvalidArgument;
+  if (datatype < 0 || datatype >= nexrNumTypes || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2)
+    return nexrInvalidArgument;
+  if (devRedOp < 0 || devRedOp >= nexrNumDevRedOps) return nexrInvalidArgument;
+  if (devRedOp == nexrDevSumPostDiv && !isInteger(datatype)) return nexrInvalidArgument;
+  if (devRedOp == nexrDevSumPostDiv && isSignedInt(datatype) && typeSize(datatype) == 1) {
+    uint32_t divisor = (uint32_t)(redOpArg >> 1);
+    if (divisor == 0) divisor = 1;
+    if ((int8_t)divisor == 0) return nexrInvalidArgument;
+  }
+  if ((nRecv && (!recvWire || !recvFlags)) || (nSend && (!sendWire || !sendFlags))) return nexrInvalidArgument;
+  if (nElts == 0) return nexrSuccess;
+  LL128Params a;
+  memset(&a, 0, sizeof(a));
+  for (int i = 0; i < nRecv; i++) {
+    if (!recvWire[i] || ((uintptr_t)recvWire[i] & 15)) return nexrInvalidArgument;
+    a.recv[i] = (const char*)recvWire[i];
+    a.recvFlag[i] = recvFlags[i];
+  }
+  for (int i = 0; i < nSend; i++) {
+    if (!sendWire[i] || ((uintptr_t)sendWire[i] & 15)) return nexrInvalidArgument;
+    a.send[i] = (char*)sendWire[i];
+    a.sendFlag[i] = sendFlags[i];
+  }
+  a.src = (const char*)src;
+  a.dst = (char*)dst;
+  a.nElts = nElts;
+  a.redArg = redOpArg;
+  a.status = status;
+  a.timeoutTicks = (uint64_t)(timeoutUs ? timeoutUs : 1000000u) * 100u;
+  a.nRecv = nRecv;
+  a.nSend = nSend;
+  a.srcIsInput = srcIsInput ? 1 : 0;
+  a.postOp = postOp ? 1 : 0;
+  const uint64_t nUnits = (nElts * typeSize(datatype) + kLL128SliceData - 1) / kLL128SliceData * 128;
+  uint64_t grid = (nUnits + kBlock - 1) / kBlock;
+  if (grid > (1u << 20)) grid = 1u << 20;
+  NEXR_HIP(launch_ll128(datatype, a, devRedOp, (int)grid, (hipStream_t)stream));
+  return nexrSuccess;
+}
+
 NEXR_API size_t nexrTypeSize(int datatype) { return typeSize(datatype); }
 
 NEXR_API const char* nexrGetErrorString(nexrResult_t result) {

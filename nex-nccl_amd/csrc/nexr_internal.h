@@ -48,6 +48,25 @@ struct LLParams {
 };
 hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s);
 
+// Launch parameters of one LL128-protocol step (nexr_ll.hip; reference src/device/prims_ll128.h).
+// Wire: 2 KiB slices of 16 x 128-B lines carrying 1920 data bytes; word 15 of every line is the flag.
+constexpr int kLL128SliceBytes = 2048;
+constexpr int kLL128SliceData = 1920;
+struct LL128Params {
+  const char* src;
+  const char* recv[NEXR_MAX_SRCS];
+  uint64_t recvFlag[NEXR_MAX_SRCS];
+  char* dst;
+  char* send[NEXR_MAX_DSTS];
+  uint64_t sendFlag[NEXR_MAX_DSTS];
+  uint64_t nElts;
+  uint64_t redArg;
+  uint32_t* status;
+  uint64_t timeoutTicks;
+  int nRecv, nSend, srcIsInput, postOp;
+};
+hipError_t launch_ll128(int dt, const LL128Params& a, int op, int grid, hipStream_t s);
+
 // Launch geometry chosen by the host.
 struct Geometry {
   int grid;

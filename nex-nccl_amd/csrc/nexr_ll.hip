@@ -152,4 +152,133 @@ hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s)
   return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------------
+// LL128 (reference src/device/prims_ll128.h:86-331). The reference moves a 2 KiB wire slice per
+// warp-32: lane wid holds regs[2g..2g+1] = user 16-B chunk ix(g, wid) = g*32 - 4*(g/2) + wid -
+// (g%2)*(wid/8) and sends them as wire words 64g + 2wid (+1); lanes wid%8 == 7 carry the line flag
+// in their odd word and therefore only half a chunk per g (the other half moved to g+1 by
+// loadRegsFinish). Here one lane owns one 16-byte wire UNIT q = 32g + wid of a slice and derives
+// which user bytes it carries from that same map, so the wire is byte-identical to the reference's
+// while the kernel itself is laid out for 64-wide waves (any number of slices per workgroup).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool wait_flag64(const char* p, uint64_t flag, uint64_t timeoutTicks, uint32_t* status) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_sys(p) != flag) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
+      if (status) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+template <int D, int OP, bool IsMin>
+__device__ __forceinline__ void ll128_unit(const LL128Params& a, uint64_t unit) {
+  using T = Ty<D>;
+  using V = typename T::V;
+  constexpr int esz = 16 / T::EPP;
+  const uint64_t slice = unit >> 7;
+  const int q = (int)(unit & 127);
+  const int g = q >> 5, wid = q & 31;
+  const bool flagLane = (wid & 7) == 7;
+  const uint64_t nBytes = a.nElts * esz;
+  const uint64_t dBase = slice * kLL128SliceData;
+  const uint64_t eltBytes = nBytes - dBase < kLL128SliceData ? nBytes - dBase : kLL128SliceData;
+  uint64_t off, len;
+  if (!flagLane) {
+    off = (uint64_t)(g * 32 - 4 * (g / 2) + wid - (g % 2) * (wid / 8)) * 16;
+    len = 16;
+  } else {
+    const int ge = g & ~1;  // the chunk loaded at the even g; odd g carries its second half
+    off = (uint64_t)(ge * 32 - 4 * (ge / 2) + wid) * 16 + (g & 1) * 8;
+    len = 8;
+  }
+  const uint64_t valid = off < eltBytes ? (eltBytes - off < len ? eltBytes - off : len) : 0;
+  const uint64_t wireOff = slice * kLL128SliceBytes + (uint64_t)q * 16;
+  const uint64_t flagOff = slice * kLL128SliceBytes + (uint64_t)(4 * g + wid / 8) * 128 + 120;
+
+  u32x4 d = (u32x4)0u;
+  if (a.src) {
+    if (valid == 16 && (((uintptr_t)(a.src + dBase + off)) & 15) == 0) d = *(const g_cu32x4*)(a.src + dBase + off);
+    else if (valid) __builtin_memcpy(&d, a.src + dBase + off, valid);
+    if constexpr (OP == nexrDevPreMulSum) {
+      if (a.srcIsInput) d = bc<u32x4>(T::mul(bc<V>(d), T::splat(a.redArg)));
+    }
+  }
+  for (int i = 0; i < NEXR_MAX_SRCS; i++) {
+    if (i >= a.nRecv) break;
+    if (!wait_flag64(a.recv[i] + flagOff, a.recvFlag[i], a.timeoutTicks, a.status)) return;
+    const uint64_t lo = ld_sys(a.recv[i] + wireOff), hi = ld_sys(a.recv[i] + wireOff + 8);
+    const u32x4 peer = (u32x4){(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    if (i == 0 && !a.src) d = peer;
+    else d = bc<u32x4>(reduce_step<D, OP, IsMin>(bc<V>(peer), bc<V>(d)));
+  }
+  if constexpr (OP == nexrDevSumPostDiv) {
+    if (a.postOp) d = bc<u32x4>(T::divide(bc<V>(d), a.redArg));
+  }
+  if constexpr (D == nexrFloat16) {
+    const bool arith = (a.nRecv >= 1 && a.src) || a.nRecv >= 2 || (OP == nexrDevPreMulSum && a.src && a.srcIsInput);
+    if (arith) d = bc<u32x4>(T::canon(bc<V>(d)));
+  }
+  const uint64_t lo = ((uint64_t)d.y << 32) | d.x, hi = ((uint64_t)d.w << 32) | d.z;
+  for (int i = 0; i < NEXR_MAX_DSTS; i++) {
+    if (i >= a.nSend) break;
+    st_sys(a.send[i] + wireOff, lo);
+    st_sys(a.send[i] + wireOff + 8, flagLane ? a.sendFlag[i] : hi);
+  }
+  if (a.dst && valid) {
+    if (valid == 16 && (((uintptr_t)(a.dst + dBase + off)) & 15) == 0) *(g_u32x4*)(a.dst + dBase + off) = d;
+    else __builtin_memcpy(a.dst + dBase + off, &d, valid);
+  }
+}
+
+template <int D, int OP>
+__global__ __launch_bounds__(kBlock) void reduce_copy_ll128_kernel(LL128Params a) {
+  const uint64_t nSlices = (a.nElts * (16 / Ty<D>::EPP) + kLL128SliceData - 1) / kLL128SliceData;
+  const uint64_t nUnits = nSlices * 128;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x; u < nUnits; u += stride) {
+    if constexpr (OP == nexrDevMinMax) {
+      if ((a.redArg & 1) == 0) ll128_unit<D, OP, true>(a, u);
+      else ll128_unit<D, OP, false>(a, u);
+    } else {
+      ll128_unit<D, OP, false>(a, u);
+    }
+  }
+}
+
+template <int D>
+static hipError_t launch_ll128_dt(const LL128Params& a, int op, int grid, hipStream_t s) {
+  const void* fn = nullptr;
+  switch (op) {
+    case nexrDevSum: fn = (const void*)&reduce_copy_ll128_kernel<D, nexrDevSum>; break;
+    case nexrDevProd: fn = (const void*)&reduce_copy_ll128_kernel<D, nexrDevProd>; break;
+    case nexrDevMinMax: fn = (const void*)&reduce_copy_ll128_kernel<D, nexrDevMinMax>; break;
+    case nexrDevPreMulSum: fn = (const void*)&reduce_copy_ll128_kernel<D, nexrDevPreMulSum>; break;
+    case nexrDevSumPostDiv:
+      if constexpr (Ty<D>::kIsInt) fn = (const void*)&reduce_copy_ll128_kernel<D, nexrDevSumPostDiv>;
+      break;
+  }
+  if (!fn) return hipErrorInvalidValue;
+  void* args[] = {const_cast<LL128Params*>(&a)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+}
+
+hipError_t launch_ll128(int dt, const LL128Params& a, int op, int grid, hipStream_t s) {
+  switch (dt) {
+    case nexrInt8: return launch_ll128_dt<nexrInt8>(a, op, grid, s);
+    case nexrUint8: return launch_ll128_dt<nexrUint8>(a, op, grid, s);
+    case nexrInt32: return launch_ll128_dt<nexrInt32>(a, op, grid, s);
+    case nexrUint32: return launch_ll128_dt<nexrUint32>(a, op, grid, s);
+    case nexrInt64: return launch_ll128_dt<nexrInt64>(a, op, grid, s);
+    case nexrUint64: return launch_ll128_dt<nexrUint64>(a, op, grid, s);
+    case nexrFloat16: return launch_ll128_dt<nexrFloat16>(a, op, grid, s);
+    case nexrFloat32: return launch_ll128_dt<nexrFloat32>(a, op, grid, s);
+    case nexrFloat64: return launch_ll128_dt<nexrFloat64>(a, op, grid, s);
+    case nexrBfloat16: return launch_ll128_dt<nexrBfloat16>(a, op, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 }  // namespace nexr

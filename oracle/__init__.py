@@ -135,3 +135,42 @@ def make_ll_lines(data: np.ndarray, flag: int) -> np.ndarray:
     lines[:, 2] = words[:, 1]
     lines[:, 3] = flag
     return lines.reshape(-1).view(np.uint8)
+
+
+LL128_SLICE_BYTES = 2048
+LL128_SLICE_DATA = 1920
+
+
+def reduce_copy_ll128(src, src_is_input, recv_wires, recv_flags, with_dst, n_send, send_flags, n_elts, datatype,
+                      dev_red_op, red_op_arg=0, post_op=False):
+    """One LL128 step on numpy buffers (wire: uint8 arrays of 2 KiB slices). Returns (rc, dst, sends)."""
+    L = lib()
+    if not hasattr(L, "_ll128_ready"):
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        P = ctypes.POINTER
+        L.oracle_reduce_copy_ll128.argtypes = [vp, ctypes.c_int, ctypes.c_int, P(vp), P(u64), vp, ctypes.c_int,
+                                               P(vp), P(u64), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_uint64, ctypes.c_int]
+        L.oracle_reduce_copy_ll128.restype = ctypes.c_int
+        L._ll128_ready = True
+    esz = L.oracle_type_size(int(datatype))
+    n_slices = (n_elts * esz + LL128_SLICE_DATA - 1) // LL128_SLICE_DATA
+    dst = np.zeros(n_elts * esz, dtype=np.uint8) if with_dst else None
+    sends = [np.zeros(n_slices * LL128_SLICE_BYTES, dtype=np.uint8) for _ in range(n_send)]
+    rw = (ctypes.c_void_p * max(1, len(recv_wires)))(*[x.ctypes.data for x in recv_wires])
+    rf = (ctypes.c_uint64 * max(1, len(recv_flags)))(*recv_flags)
+    sw = (ctypes.c_void_p * max(1, n_send))(*[x.ctypes.data for x in sends])
+    sf = (ctypes.c_uint64 * max(1, len(send_flags)))(*send_flags)
+    rc = L.oracle_reduce_copy_ll128(src.ctypes.data if src is not None else None, 1 if src_is_input else 0,
+                                    len(recv_wires), rw, rf, dst.ctypes.data if dst is not None else None, n_send, sw,
+                                    sf, int(n_elts), int(datatype), int(dev_red_op),
+                                    int(red_op_arg) & 0xFFFFFFFFFFFFFFFF, 1 if post_op else 0)
+    return rc, dst, sends
+
+
+def make_ll128_wire(data: np.ndarray, flag: int, datatype: int) -> np.ndarray:
+    """Encode data into LL128 wire slices via the oracle (a send-only step)."""
+    n = data.size
+    rc, _, sends = reduce_copy_ll128(np.ascontiguousarray(data), False, [], [], False, 1, [flag], n, datatype, 0)
+    assert rc == 0
+    return sends[0]

@@ -401,6 +401,101 @@ int oracle_reduce_copy_ll(const void* src, int srcIsInput, int nRecv, const void
   return R_OK;
 }
 
+/* ---- LL128 protocol step (reference src/device/prims_ll128.h:86-331) --------------------------- */
+/* Restated literally from the warp-32 register flow: per 2 KiB wire slice (WireWordPerSlice = 32
+ * lanes x 8 u64), 1920 data bytes (DataEltPerSlice); lane `wid` holds regs[0..7]; user 16-B chunk
+ * ix = g*32 - 4*(g/2) + wid - (g%2)*(wid/8) goes to regs[2g..2g+1] (loadRegsBegin :86-131); flag
+ * lanes (wid%8 == 7) load only even g and move regs[2g-1] -> regs[2g] (loadRegsFinish :133-140);
+ * regs[u], regs[u+1] travel as wire words u*32 + 2*wid (+1), the flag lane's odd word carrying the
+ * flag (recvReduceSendCopy :184-292); storeRegs (:142-174) reverses the permutation. */
+static void ll128_words(int dt, const Fn* fn, int op, uint64_t* w, int n, const uint8_t* peerW, int mode) {
+  /* mode 0: w = peer; 1: w = op(peer, w); applied per element of each u64 */
+  (void)op;
+  const size_t esz = oracle_type_size(dt);
+  for (int k = 0; k < n; k++) {
+    if (mode == 0) { memcpy(&w[k], peerW + 8 * k, 8); continue; }
+    uint8_t* x = (uint8_t*)&w[k];
+    for (size_t e = 0; e < 8 / esz; e++) elem_reduce(dt, fn, peerW + 8 * k + e * esz, x + e * esz, x + e * esz);
+  }
+}
+
+int oracle_reduce_copy_ll128(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
+                             const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
+                             const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp, uint64_t redOpArg,
+                             int postOp) {
+  int r = check(1, 0, datatype, devRedOp, redOpArg, 0, NULL);
+  if (r != R_OK) return r;
+  if (nRecv < 0 || nRecv > 8 || nSend < 0 || nSend > 8 || (!src && !nRecv) || (!dst && !nSend)) return R_INVALID;
+  Fn fn;
+  make_fn(&fn, devRedOp, redOpArg);
+  const size_t esz = oracle_type_size(datatype);
+  const size_t nBytes = nElts * esz;
+  const size_t nSlices = (nBytes + 1919) / 1920;
+  for (size_t sl = 0; sl < nSlices; sl++) {
+    const size_t dBase = sl * 1920, wBase = sl * 256;                 /* bytes / u64 words */
+    const size_t eltBytes = nBytes - dBase < 1920 ? nBytes - dBase : 1920;
+    /* 1. every lane waits for its lines' flags (needReload over all u, :193-206) */
+    for (int i = 0; i < nRecv; i++)
+      for (int wid = 7; wid < 32; wid += 8)
+        for (int u = 0; u < 8; u += 2) {
+          uint64_t f;
+          memcpy(&f, (const uint8_t*)recvWire[i] + 8 * (wBase + u * 32 + 2 * wid + 1), 8);
+          if (f != recvFlags[i]) return 3;
+        }
+    for (int wid = 0; wid < 32; wid++) {
+      const int flagThread = (wid % 8) == 7;
+      uint64_t v[8] = {0};
+      if (src) {
+        for (int g = 0; g < 4; g++) {
+          int ix = g * 32 - 4 * (g / 2) + wid - (g % 2) * (wid / 8);
+          if ((!flagThread || g % 2 == 0) && (size_t)ix * 16 < eltBytes) {
+            size_t nb = eltBytes - (size_t)ix * 16 < 16 ? eltBytes - (size_t)ix * 16 : 16;
+            memcpy(&v[2 * g], (const uint8_t*)src + dBase + (size_t)ix * 16, nb);
+          }
+        }
+        for (int g = 1; g < 4; g += 2)
+          if (flagThread) v[2 * g] = v[2 * g - 1];
+        if (devRedOp == OP_PREMULSUM && srcIsInput)
+          for (int u = 0; u < 8; u += 2) {
+            for (size_t e = 0; e < 8 / esz; e++) elem_premul(datatype, redOpArg, (uint8_t*)&v[u] + e * esz);
+            if (!flagThread)
+              for (size_t e = 0; e < 8 / esz; e++) elem_premul(datatype, redOpArg, (uint8_t*)&v[u + 1] + e * esz);
+          }
+      }
+      for (int i = 0; i < nRecv; i++) {
+        for (int u = 0; u < 8; u += 2) {
+          const uint8_t* wp = (const uint8_t*)recvWire[i] + 8 * (wBase + u * 32 + 2 * wid);
+          ll128_words(datatype, &fn, devRedOp, &v[u], 2, wp, (i == 0 && !src) ? 0 : 1);
+        }
+      }
+      if (devRedOp == OP_SUMPOSTDIV && postOp)
+        for (int u = 0; u < 8; u++)
+          for (size_t e = 0; e < 8 / esz; e++) elem_postdiv(datatype, &fn, (uint8_t*)&v[u] + e * esz);
+      for (int i = 0; i < nSend; i++)
+        for (int u = 0; u < 8; u += 2) {
+          uint8_t* wp = (uint8_t*)sendWire[i] + 8 * (wBase + u * 32 + 2 * wid);
+          uint64_t hi = flagThread ? sendFlags[i] : v[u + 1];
+          memcpy(wp, &v[u], 8);
+          memcpy(wp + 8, &hi, 8);
+        }
+      if (dst) {
+        uint64_t w[8];
+        memcpy(w, v, sizeof(w));
+        for (int g = 1; g < 4; g += 2)
+          if (flagThread) w[2 * g - 1] = w[2 * g];
+        for (int g = 0; g < 4; g++) {
+          int ix = g * 32 - 4 * (g / 2) + wid - (g % 2) * (wid / 8);
+          if ((!flagThread || g % 2 == 0) && (size_t)ix * 16 < eltBytes) {
+            size_t nb = eltBytes - (size_t)ix * 16 < 16 ? eltBytes - (size_t)ix * 16 : 16;
+            memcpy((uint8_t*)dst + dBase + (size_t)ix * 16, &w[2 * g], nb);
+          }
+        }
+      }
+    }
+  }
+  return R_OK;
+}
+
 /* The LL step with the nexrReduceCopyLLFn signature (include/nexr_ring.h): lets tests run the LL
  * ring schedule on CPU. A not-ready line (flag mismatch) reports through *status like the kernel. */
 int oracle_reduce_copy_ll_fn(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
