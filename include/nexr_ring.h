@@ -12,7 +12,8 @@
  *     (src/include/collectives.h:17-18),
  *   - or, with protocol = LL, LLGenericOp's one-step-per-call credits and line flags
  *     NCCL_LL_FLAG(step+1) (src/device/prims_ll.h:55-93, :218-283; chunk = stepSize/2,
- *     src/enqueue.cc:1997),
+ *     src/enqueue.cc:1997); with LL128, GenericOp's steps and 64-bit line flags step+1
+ *     (src/device/prims_ll128.h:55-85, :294-331; chunk = stepSize*15/16, enqueue.cc:1998),
  *   - the host chunking for ring SIMPLE (src/enqueue.cc:1993-1996: chunkSize = stepSize * 4),
  *   - ncclLaunchOneRank for nRanks == 1 (src/device/onerank.cc:48-83),
  *   - op encoding through nexrHostToDevRedOp (src/enqueue.cc:2185-2278).
@@ -41,20 +42,28 @@ typedef nexrResult_t (*nexrReduceCopyLLFn)(const void* src, int srcIsInput, int 
                                            uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
                                            nexrStream_t stream);
 
+/* Same signature as nexrReduceCopyLL128. */
+typedef nexrResult_t (*nexrReduceCopyLL128Fn)(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
+                                              const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
+                                              const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
+                                              uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
+                                              nexrStream_t stream);
+
 typedef enum { nexrRingHostMemory = 0, nexrRingDeviceMemory = 1 } nexrRingMemMode_t;
 /* The two protocols the emulated ring restates (the reference's NCCL_PROTO_SIMPLE / NCCL_PROTO_LL).
  * Numbered so that a zero-initialised config selects SIMPLE. */
-typedef enum { nexrRingProtoSimple = 0, nexrRingProtoLL = 1 } nexrRingProto_t;
+typedef enum { nexrRingProtoSimple = 0, nexrRingProtoLL = 1, nexrRingProtoLL128 = 2 } nexrRingProto_t;
 
 typedef struct {
   int nRanks;          /* emulated ranks (threads), >= 1 */
   size_t buffBytes;    /* per-connection buffer (NCCL_BUFFSIZE); 0 = the protocol default: 4 MiB
-                          SIMPLE, 512 KiB LL (src/init.cc:618-631) */
+                          SIMPLE, 512 KiB LL, 4,915,200 B LL128 (src/init.cc:618-631) */
   int memMode;         /* nexrRingMemMode_t: where user buffers and FIFOs live */
   nexrReduceCopyFn fn; /* SIMPLE: NULL = nexrReduceCopyHost (host) / nexrReduceCopy (device) */
   int timeoutMs;       /* spin-wait bound per FIFO wait; 0 = 60000 */
   int protocol;        /* nexrRingProto_t (0 = SIMPLE) */
   nexrReduceCopyLLFn llFn; /* LL: NULL = nexrReduceCopyLL (device memory mode only) */
+  nexrReduceCopyLL128Fn ll128Fn; /* LL128: NULL = nexrReduceCopyLL128 (device memory mode only) */
 } nexrRingConfig;
 
 typedef struct nexrRingComm* nexrRingComm_t;

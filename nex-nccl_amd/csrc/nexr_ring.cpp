@@ -23,6 +23,7 @@ constexpr int kChunkSteps = kSteps / 2;                  // ALLREDUCE_CHUNKSTEPS
 constexpr int kSlicePerChunk = kChunkSteps / kSliceSteps;
 constexpr size_t kDefaultBuffBytes = 4u << 20;           // NCCL_BUFFSIZE default (init.cc:620-634)
 constexpr size_t kDefaultLLBuffBytes = 8 * 512 * kSteps * 16;  // DEFAULT_LL_BUFFSIZE (init.cc:618)
+constexpr size_t kDefaultLL128BuffBytes = 120 * 640 * kSteps * 8;  // DEFAULT_LL128_BUFFSIZE (init.cc:619)
 
 // One directed connection prev -> r. The FIFO belongs to the receiver (the sender writes into it,
 // like a P2P/SHM transport's recv buffer, src/include/device.h:753-771).
@@ -46,7 +47,8 @@ struct nexrRingComm {
   std::vector<int> devices;
   std::vector<hipStream_t> streams;
   std::vector<uint32_t*> status;     // LL: per-rank pinned status word the kernel reports timeouts in
-  bool ll = false;
+  bool ll = false;     // LL or LL128: one FIFO step per primitive call, data readiness in line flags
+  int proto = nexrRingProtoSimple;
   bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
   bool broken = false;
 };
@@ -78,6 +80,7 @@ struct Prims {
   uint64_t redOpArgs[1];
   nexrReduceCopyFn fn;
   nexrReduceCopyLLFn llFn;
+  nexrReduceCopyLL128Fn ll128Fn;
   uint32_t* status;
   hipStream_t stream;
   bool device;
@@ -178,10 +181,18 @@ struct Prims {
       const uint32_t recvFlag[1] = {(uint32_t)(rs + 1)};  // NCCL_LL_FLAG(recvStep+1)
       const uint32_t sendFlag[1] = {(uint32_t)(ss + 1)};
       if (status) *status = 0;
-      nexrResult_t r = llFn(Src ? userInput + srcIx * esz : nullptr, Src ? 1 : 0, Recv ? 1 : 0, recvLines, recvFlag,
-                            Dst ? userOutput + dstIx * esz : nullptr, Send ? 1 : 0, sendLines, sendFlag,
-                            (size_t)nelem, datatype, devOp, redOpArgs[0], postOp ? 1 : 0, status,
-                            (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u), (nexrStream_t)stream);
+      const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
+      nexrResult_t r;
+      if (c->proto == nexrRingProtoLL128) {  // 64-bit flags = step + 1 (prims_ll128.h:49-50)
+        const uint64_t rf[1] = {rs + 1}, sf[1] = {ss + 1};
+        r = ll128Fn(Src ? userInput + srcIx * esz : nullptr, Src ? 1 : 0, Recv ? 1 : 0, recvLines, rf,
+                    Dst ? userOutput + dstIx * esz : nullptr, Send ? 1 : 0, sendLines, sf, (size_t)nelem, datatype,
+                    devOp, redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
+      } else {
+        r = llFn(Src ? userInput + srcIx * esz : nullptr, Src ? 1 : 0, Recv ? 1 : 0, recvLines, recvFlag,
+                 Dst ? userOutput + dstIx * esz : nullptr, Send ? 1 : 0, sendLines, sendFlag, (size_t)nelem,
+                 datatype, devOp, redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
+      }
       if (r == nexrSuccess && device && hipStreamSynchronize(stream) != hipSuccess) r = nexrUnhandledCudaError;
       if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
       if (r != nexrSuccess) {
@@ -216,8 +227,12 @@ struct Prims {
 // channelCount = count, chunkCount = chunkSize / sizeof(T): enqueue.cc:1993-1996, :655-678).
 void runRing(Prims& p, int nranks, int64_t count) {
   const int ringIx = p.rank;
-  // SIMPLE: chunkSize = stepSize * chunkSteps; LL: stepSize / 2 (enqueue.cc:1993-1997)
-  int64_t chunkCount = p.c->ll ? (int64_t)(p.c->stepBytes / 2 / p.esz) : (int64_t)(p.c->stepBytes * kChunkSteps / p.esz);
+  // SIMPLE: chunkSize = stepSize * chunkSteps; LL: stepSize / 2; LL128: stepSize / 16 * 15, aligned
+  // to the 1920-B grain (enqueue.cc:1993-1999, :2062)
+  int64_t chunkBytes = (int64_t)(p.c->stepBytes * kChunkSteps);
+  if (p.c->proto == nexrRingProtoLL) chunkBytes = (int64_t)(p.c->stepBytes / 2);
+  if (p.c->proto == nexrRingProtoLL128) chunkBytes = (int64_t)(p.c->stepBytes / 16 * 15) / 1920 * 1920;
+  int64_t chunkCount = chunkBytes / (int64_t)p.esz;
   const int64_t loopCount = nranks * chunkCount;
   auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
   for (int64_t elemOffset = 0; elemOffset < count; elemOffset += loopCount) {
@@ -262,6 +277,13 @@ nexrResult_t defaultLLFn(const void* src, int srcIsInput, int nRecv, const void*
   return nexrReduceCopyLL(src, srcIsInput, nRecv, recvLines, recvFlags, dst, nSend, sendLines, sendFlags, n, dt, op,
                           arg, post, status, timeoutUs, s);
 }
+nexrResult_t defaultLL128Fn(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
+                            const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
+                            const uint64_t* sendFlags, size_t n, int dt, int op, uint64_t arg, int post,
+                            uint32_t* status, uint32_t timeoutUs, nexrStream_t s) {
+  return nexrReduceCopyLL128(src, srcIsInput, nRecv, recvWire, recvFlags, dst, nSend, sendWire, sendFlags, n, dt, op,
+                             arg, post, status, timeoutUs, s);
+}
 nexrResult_t defaultDeviceFn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t n, int dt,
                              int op, uint64_t arg, int nPre, const uint64_t* pre, int post, nexrStream_t s) {
   return nexrReduceCopy(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
@@ -274,20 +296,28 @@ extern "C" {
 NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConfig* cfg) {
   if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024) return nexrInvalidArgument;
   if (cfg->memMode != nexrRingHostMemory && cfg->memMode != nexrRingDeviceMemory) return nexrInvalidArgument;
-  if (cfg->protocol != nexrRingProtoSimple && cfg->protocol != nexrRingProtoLL) return nexrInvalidArgument;
-  // The LL kernel polls live FIFO lines: it needs device-visible lines, i.e. device memory, unless
-  // the caller supplies its own LL implementation (e.g. a CPU checker).
-  if (cfg->protocol == nexrRingProtoLL && cfg->memMode == nexrRingHostMemory && !cfg->llFn) return nexrInvalidUsage;
+  if (cfg->protocol != nexrRingProtoSimple && cfg->protocol != nexrRingProtoLL && cfg->protocol != nexrRingProtoLL128)
+    return nexrInvalidArgument;
+  // The LL/LL128 kernels poll live FIFO lines: they need device-visible lines, i.e. device memory,
+  // unless the caller supplies its own step implementation (e.g. a CPU checker).
+  if (cfg->memMode == nexrRingHostMemory && ((cfg->protocol == nexrRingProtoLL && !cfg->llFn) ||
+                                             (cfg->protocol == nexrRingProtoLL128 && !cfg->ll128Fn)))
+    return nexrInvalidUsage;
   auto* c = new nexrRingComm();
   c->cfg = *cfg;
-  c->ll = cfg->protocol == nexrRingProtoLL;
-  if (c->cfg.buffBytes == 0) c->cfg.buffBytes = c->ll ? kDefaultLLBuffBytes : kDefaultBuffBytes;
-  if (c->cfg.buffBytes % (kSteps * 16) != 0) {
+  c->proto = cfg->protocol;
+  c->ll = cfg->protocol != nexrRingProtoSimple;
+  if (c->cfg.buffBytes == 0)
+    c->cfg.buffBytes = c->proto == nexrRingProtoLL ? kDefaultLLBuffBytes
+                       : c->proto == nexrRingProtoLL128 ? kDefaultLL128BuffBytes : kDefaultBuffBytes;
+  if (c->cfg.buffBytes % (kSteps * 16) != 0 ||
+      (c->proto == nexrRingProtoLL128 && c->cfg.buffBytes % (kSteps * 2048) != 0)) {  // whole LL128 slices
     delete c;
     return nexrInvalidArgument;
   }
   if (!c->cfg.fn) c->cfg.fn = cfg->memMode == nexrRingDeviceMemory ? defaultDeviceFn : defaultHostFn;
   if (!c->cfg.llFn) c->cfg.llFn = defaultLLFn;
+  if (!c->cfg.ll128Fn) c->cfg.ll128Fn = defaultLL128Fn;
   c->stepBytes = c->cfg.buffBytes / kSteps;
   const int n = cfg->nRanks;
   c->recvStep.assign(n, 0);
@@ -296,7 +326,8 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   c->streams.assign(n, nullptr);
   c->status.assign(n, nullptr);
   int nDev = 0;
-  const bool needHip = cfg->memMode == nexrRingDeviceMemory || (!c->ll && !cfg->fn) || (c->ll && !cfg->llFn);
+  const bool needHip = cfg->memMode == nexrRingDeviceMemory || (c->proto == nexrRingProtoSimple && !cfg->fn) ||
+                       (c->proto == nexrRingProtoLL && !cfg->llFn) || (c->proto == nexrRingProtoLL128 && !cfg->ll128Fn);
   c->pinnedStatus = needHip;
   if (needHip) {
     if (hipGetDeviceCount(&nDev) != hipSuccess || nDev < 1) {
@@ -412,6 +443,7 @@ NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sen
       p.redOpArgs[0] = red.scalarArg;
       p.fn = c->cfg.fn;
       p.llFn = c->cfg.llFn;
+      p.ll128Fn = c->cfg.ll128Fn;
       p.status = c->status[rank];
       p.stream = c->streams[rank];
       p.device = device;

@@ -20,6 +20,7 @@ HOST_MEMORY = 0
 DEVICE_MEMORY = 1
 PROTO_SIMPLE = 0
 PROTO_LL = 1
+PROTO_LL128 = 2
 
 REDUCE_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
@@ -30,7 +31,7 @@ REDUCE_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(cty
 class RingConfig(ctypes.Structure):
     _fields_ = [("nRanks", ctypes.c_int), ("buffBytes", ctypes.c_size_t), ("memMode", ctypes.c_int),
                 ("fn", ctypes.c_void_p), ("timeoutMs", ctypes.c_int), ("protocol", ctypes.c_int),
-                ("llFn", ctypes.c_void_p)]
+                ("llFn", ctypes.c_void_p), ("ll128Fn", ctypes.c_void_p)]
 
 
 _ring = None
@@ -59,9 +60,9 @@ class RingComm:
 
     def __init__(self, n_ranks: int, mem_mode: int = HOST_MEMORY, buff_bytes: int = 0,
                  fn_address: Optional[int] = None, timeout_ms: int = 0, protocol: int = PROTO_SIMPLE,
-                 ll_fn_address: Optional[int] = None):
+                 ll_fn_address: Optional[int] = None, ll128_fn_address: Optional[int] = None):
         cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms, protocol,
-                         ll_fn_address or None)
+                         ll_fn_address or None, ll128_fn_address or None)
         h = ctypes.c_void_p()
         _check(ring_lib().nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
         self._h = h

@@ -513,6 +513,21 @@ int oracle_reduce_copy_ll_fn(const void* src, int srcIsInput, int nRecv, const v
   return r;
 }
 
+int oracle_reduce_copy_ll128_fn(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
+                                const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
+                                const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
+                                uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs, void* stream) {
+  (void)timeoutUs;
+  (void)stream;
+  int r = oracle_reduce_copy_ll128(src, srcIsInput, nRecv, recvWire, recvFlags, dst, nSend, sendWire, sendFlags, nElts,
+                                   datatype, devRedOp, redOpArg, postOp);
+  if (r == 3) {
+    if (status) *status = 1;
+    return R_OK;
+  }
+  return r;
+}
+
 /* hostToDevRedOp restated (reference src/enqueue.cc:2185-2278), built-in ops only.
  * out[0] = devRedOp, out[1] = scalarArg. Returns 0 or 4. */
 int oracle_host_to_dev_redop(int op, int datatype, int nRanks, uint64_t* out) {

@@ -66,10 +66,13 @@ def ring_allreduce_expected(inputs, datatype: int, op: int, buff_bytes: int = 4 
     return [out.copy() for _ in range(n)]
 
 
-def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int = 8 * 512 * 8 * 16):
-    """The LL-protocol ring: same runRing schedule (chunk = stepBytes/2, src/enqueue.cc:1997), but
-    every step folds with the received PEER partial as the first operand (prims_ll.h:251-258)."""
-    from . import make_ll_lines, reduce_copy_ll
+def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int = 8 * 512 * 8 * 16,
+                               proto: str = "ll"):
+    """The LL / LL128-protocol ring: same runRing schedule (chunk = stepBytes/2 for LL,
+    stepBytes/16*15 on the 1920-B grain for LL128, src/enqueue.cc:1997-1999), but every step folds
+    with the received PEER partial as the first operand (prims_ll.h:251-258, prims_ll128.h:214-219)."""
+    from . import reduce_copy_ll, reduce_copy_ll128
+    step = reduce_copy_ll if proto == "ll" else reduce_copy_ll128
     n = len(inputs)
     enc = host_to_dev_red_op(op, datatype, n)
     if enc is None:
@@ -80,7 +83,10 @@ def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int =
     if count == 0 or n == 1:
         return ring_allreduce_expected(inputs, datatype, op)
     out = np.empty_like(inputs[0])
-    chunk = (buff_bytes // 8) // 2 // esz
+    if proto == "ll":
+        chunk = (buff_bytes // 8) // 2 // esz
+    else:
+        chunk = (buff_bytes // 8) // 16 * 15 // 1920 * 1920 // esz
     loop = n * chunk
     for elem_off in range(0, count, loop):
         rem = count - elem_off
@@ -93,12 +99,12 @@ def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int =
                 continue
             m = hi - lo
             r = (c + 1) % n
-            rc, _, sends = reduce_copy_ll(inputs[r][lo:hi], True, [], [], False, 1, [1], m, datatype, dev_op, arg)
+            rc, _, sends = step(inputs[r][lo:hi], True, [], [], False, 1, [1], m, datatype, dev_op, arg)
             for k in range(2, n + 1):
                 r = (c + k) % n
                 post = k == n
-                rc, dst, sends = reduce_copy_ll(inputs[r][lo:hi], True, [sends[0]], [1], post, 1, [1], m, datatype,
-                                                dev_op, arg, post)
+                rc, dst, sends = step(inputs[r][lo:hi], True, [sends[0]], [1], post, 1, [1], m, datatype, dev_op, arg,
+                                      post)
                 assert rc == 0
             out[lo:hi] = dst.view(out.dtype)
     return [out.copy() for _ in range(n)]

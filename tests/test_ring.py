@@ -130,3 +130,24 @@ def test_ll_ring_matches_peer_first_fold_oracle(ring, oracle, oracle_ll_fn, n_ra
 def test_ll_ring_needs_device_memory_or_a_custom_step(ring, nexr):
     with pytest.raises(nexr.NexrError):
         ring.RingComm(2, ring.HOST_MEMORY, 0, None, 0, ring.PROTO_LL, None)
+
+
+@pytest.fixture(scope="module")
+def oracle_ll128_fn(oracle):
+    return ctypes.cast(oracle.lib().oracle_reduce_copy_ll128_fn, ctypes.c_void_p).value
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3, 4])
+@pytest.mark.parametrize("dt,op,special", [(mg.F32, 0, False), (mg.BF16, 0, True), (mg.I32, 2, True),
+                                           (mg.F16, 4, True), (mg.U8, 4, True)])
+def test_ll128_ring_matches_peer_first_fold_oracle(ring, oracle, oracle_ll128_fn, n_ranks, dt, op, special):
+    from oracle.ring import ring_allreduce_expected_ll
+    buff = 8 * 2048 * 4  # 4 slices per step: many loops and credit stalls
+    count = 40_000 + 11 * n_ranks
+    inputs = mg.gen_inputs(dt, n_ranks, count, 0xC00 + dt * 7 + op, special)
+    recv = [np.zeros_like(x) for x in inputs]
+    with ring.RingComm(n_ranks, ring.HOST_MEMORY, buff, None, 20000, ring.PROTO_LL128, None, oracle_ll128_fn) as comm:
+        comm.all_reduce([a.ctypes.data for a in inputs], [b.ctypes.data for b in recv], count, dt, op)
+    exp = ring_allreduce_expected_ll(inputs, dt, op, buff, proto="ll128")
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, recv[r]) == mg.canon_bytes(dt, exp[r]), f"rank {r}"

@@ -71,3 +71,18 @@ def test_ll_ring_device_memory(ring, oracle, n_ranks, dt, op):
     exp = ring_allreduce_expected_ll(inputs, dt, op)
     for r in range(n_ranks):
         assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+@pytest.mark.parametrize("n_ranks,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 4), (4, mg.I32, 3)])
+def test_ll128_ring_device_memory(ring, oracle, n_ranks, dt, op):
+    from oracle.ring import ring_allreduce_expected_ll
+    count = (1 << 20) + 9
+    inputs = mg.gen_inputs(dt, n_ranks, count, 91 * dt + op, special=True)
+    send = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+    recv = [torch.zeros_like(s) for s in send]
+    torch.cuda.synchronize()
+    with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 0, None, 20000, ring.PROTO_LL128) as comm:
+        comm.all_reduce([s.data_ptr() for s in send], [d.data_ptr() for d in recv], count, dt, op)
+    exp = ring_allreduce_expected_ll(inputs, dt, op, 120 * 640 * 8 * 8, proto="ll128")
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
