@@ -311,3 +311,33 @@ def test_host_zero_copy_pinned_buffers(nexr, oracle, dev):
     pageable = np.zeros_like(srcs[0])
     nexr.reduce_copy_ptrs(sp, [pinned for pinned in dp[:1]] + [pageable.ctypes.data], n, mg.F16, mg.SUM, host=True)
     assert same(mg.F16, pageable, exp)
+
+
+def test_random_fuzz_against_oracle(nexr, oracle, dev):
+    # 300 random (datatype, op, K, M, n, per-pointer offsets, pre/post) cases, special values on
+    rng = np.random.default_rng(20261015)
+    ops = [("sum", mg.SUM), ("prod", mg.PROD), ("min", mg.MINMAX), ("max", mg.MINMAX), ("premulsum", mg.PREMULSUM),
+           ("sumpostdiv", mg.SUMPOSTDIV)]
+    for case in range(300):
+        dt = int(rng.choice(sorted(mg.DT_NAMES)))
+        name, op = ops[int(rng.integers(0, len(ops)))]
+        if name == "sumpostdiv" and dt not in mg.INTS:
+            name, op = "sum", mg.SUM
+        k = int(rng.integers(1, 9))
+        m = int(rng.integers(1, 9))
+        n = int(rng.choice([1, 2, 7, 15, 16, 17, 255, 1023, 4097, 65535, 300_001]))
+        esz = np.dtype(mg.STORE[dt]).itemsize
+        mode = int(rng.integers(0, 3))
+        if mode == 0:
+            so, do = [0] * k, [0] * m
+        elif mode == 1:
+            ph = int(rng.integers(0, 16 // esz)) * esz
+            so, do = [ph] * k, [ph] * m
+        else:
+            so = [int(rng.integers(0, 16)) for _ in range(k)]
+            do = [int(rng.integers(0, 16)) for _ in range(m)]
+        arg, pre, post = _case_args(dt, name, op, k, rng)
+        srcs = mg.gen_inputs(dt, k, n, 5000 + case, special=True)
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg, pre, post)[0]
+        for o in run_gpu(nexr, srcs, m, dt, op, arg, pre, post, src_off=so, dst_off=do):
+            assert same(dt, o, exp), (case, mg.DT_NAMES[dt], name, k, m, n, so, do)
