@@ -121,6 +121,35 @@ NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDs
                                      nexrStream_t stream);
 
 /*
+ * nexrReduceCopyBatch — many independent reduce-copies of one (datatype, devRedOp) in as few
+ * launches as possible: the analogue of a kernel launch carrying a batch of works in its 4 KiB
+ * argument block (reference src/include/device.h:1074-1098 ncclDevKernelArgs4K,
+ * src/device/common.h:165-200 loadWorkBatchToShmem, :424-445 the per-block work loop). Each work
+ * has exactly the semantics of one nexrReduceCopy call with its own fields. Works with the same
+ * nSrcs share a launch (at most NEXR_MAX_BATCH_WORKS per launch); each work gets workgroups in
+ * proportion to its size. Works run concurrently in no defined order, so no work's dsts may overlap
+ * another work's srcs or dsts (in-place within one work is allowed). Every work is validated
+ * before anything is launched: on an argument error nothing runs. Works with nElts == 0 or
+ * nDsts == 0 are skipped. Small messages are launch-bound (~4 us per nexrReduceCopy call on
+ * MI355X); a batch pays that once per launch.
+ */
+#define NEXR_MAX_BATCH_WORKS 14
+typedef struct {
+  int nSrcs;
+  int nDsts;
+  const void* srcs[NEXR_MAX_SRCS];
+  void* dsts[NEXR_MAX_DSTS];
+  size_t nElts;
+  uint64_t redOpArg;
+  int nPreOpSrcs;
+  int postOp;
+  uint64_t preOpArgs[NEXR_MAX_SRCS];
+} nexrReduceCopyWork;
+
+NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int devRedOp,
+                                          nexrStream_t stream);
+
+/*
  * nexrReduceCopyHost — the same reduce-copy for buffers in HOST memory (the emulated
  * transport's staging FIFOs, reference src/include/device.h:753-771): copies the K inputs
  * host->device, runs nexrReduceCopy, copies the M outputs device->host, and synchronises the

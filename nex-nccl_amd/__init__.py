@@ -76,7 +76,7 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
              DataType.Float8e5m2: 1}
 
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
-ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
+ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
                "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
 
 
@@ -94,6 +94,16 @@ class DevRedOpFull(ctypes.Structure):
     """Mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693)."""
     _fields_ = [("op", ctypes.c_int), ("proxyOp", ctypes.c_int), ("scalarArgIsPtr", ctypes.c_int),
                 ("scalarArg", ctypes.c_uint64)]
+
+
+MAX_BATCH_WORKS = 14  # NEXR_MAX_BATCH_WORKS
+
+
+class ReduceCopyWork(ctypes.Structure):
+    """Mirror of nexrReduceCopyWork (include/nexr.h): one reduce-copy of a batch."""
+    _fields_ = [("nSrcs", ctypes.c_int), ("nDsts", ctypes.c_int), ("srcs", ctypes.c_void_p * 8),
+                ("dsts", ctypes.c_void_p * 8), ("nElts", ctypes.c_size_t), ("redOpArg", ctypes.c_uint64),
+                ("nPreOpSrcs", ctypes.c_int), ("postOp", ctypes.c_int), ("preOpArgs", ctypes.c_uint64 * 8)]
 
 
 _lib = None
@@ -114,6 +124,8 @@ def lib() -> ctypes.CDLL:
         f = getattr(L, name)
         f.argtypes = [i32, P(vp), i32, P(vp), sz, i32, i32, u64, i32, P(u64), i32, vp]
         f.restype = i32
+    L.nexrReduceCopyBatch.argtypes = [P(ReduceCopyWork), i32, i32, i32, vp]
+    L.nexrReduceCopyBatch.restype = i32
     L.nexrHostToDevRedOp.argtypes = [P(DevRedOpFull), i32, i32, i32]
     L.nexrHostToDevRedOp.restype = i32
     L.nexrLaunchOneRank.argtypes = [vp, vp, sz, DevRedOpFull, i32, vp]
@@ -175,6 +187,33 @@ def reduce_copy_ptrs(srcs: Sequence[int], dsts: Sequence[int], n_elts: int, data
            int(dev_red_op), int(red_op_arg) & 0xFFFFFFFFFFFFFFFF, len(pre), _u64_array(pre),
            1 if post_op else 0, ctypes.c_void_p(int(stream)) if stream else None)
     _check(rc, "nexrReduceCopyHost" if host else "nexrReduceCopy")
+
+
+def make_work(srcs: Sequence[int], dsts: Sequence[int], n_elts: int, red_op_arg: int = 0,
+              pre_op_args: Optional[Sequence[int]] = None, post_op: bool = False) -> ReduceCopyWork:
+    """One nexrReduceCopyWork from device addresses (raises on more than 8 srcs/dsts)."""
+    pre = list(pre_op_args) if pre_op_args else []
+    if len(srcs) > 8 or len(dsts) > 8 or len(pre) > 8:
+        raise NexrError(Result.InvalidArgument, "at most 8 srcs, dsts and preOpArgs per work")
+    w = ReduceCopyWork()
+    w.nSrcs, w.nDsts, w.nElts = len(srcs), len(dsts), int(n_elts)
+    for i, a in enumerate(srcs):
+        w.srcs[i] = int(a)
+    for i, a in enumerate(dsts):
+        w.dsts[i] = int(a)
+    w.redOpArg = int(red_op_arg) & 0xFFFFFFFFFFFFFFFF
+    w.nPreOpSrcs = len(pre)
+    for i, v in enumerate(pre):
+        w.preOpArgs[i] = int(v) & 0xFFFFFFFFFFFFFFFF
+    w.postOp = 1 if post_op else 0
+    return w
+
+
+def reduce_copy_batch(works: Sequence[ReduceCopyWork], datatype: int, dev_red_op: int, stream: int = 0) -> None:
+    """``nexrReduceCopyBatch``: independent reduce-copies of one (datatype, op) in few launches."""
+    arr = (ReduceCopyWork * max(1, len(works)))(*works)
+    _check(lib().nexrReduceCopyBatch(arr, len(works), int(datatype), int(dev_red_op),
+                                     ctypes.c_void_p(int(stream)) if stream else None), "nexrReduceCopyBatch")
 
 
 def host_to_dev_red_op(op: int, datatype: int, n_ranks: int = 1) -> DevRedOpFull:

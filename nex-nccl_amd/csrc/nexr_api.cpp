@@ -125,14 +125,9 @@ void planLayout(RCParams& p, int nSrcs, size_t esz) {
   p.nPacks = (p.nElts - head) * esz / 16;
 }
 
-nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
-                              size_t nElts, int datatype, int op, uint64_t redOpArg, int nPreOpSrcs,
-                              const uint64_t* preOpArgs, const void* prePtr, int postOp, hipStream_t stream) {
-  nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, op, redOpArg, nPreOpSrcs, preOpArgs);
-  if (r != nexrSuccess) return r;
-  if (nElts == 0 || nDsts == 0) return nexrSuccess;  // common_kernel.h:288-289: nothing to store
-  const size_t esz = typeSize(datatype);
-  RCParams p;
+void fillParams(RCParams& p, int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                size_t esz, uint64_t redOpArg, int nPreOpSrcs, const uint64_t* preOpArgs, const void* prePtr,
+                int postOp) {
   memset(&p, 0, sizeof(p));
   for (int s = 0; s < nSrcs; s++) p.src[s] = (const char*)srcs[s];
   for (int d = 0; d < nDsts; d++) p.dst[d] = (char*)dsts[d];
@@ -144,9 +139,100 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   p.nPreOp = nPreOpSrcs;
   p.postOp = postOp ? 1 : 0;
   planLayout(p, nSrcs, esz);
+}
+
+// Lane work items of one reduce-copy: elements (generic path) or U-pack groups (packed path).
+uint64_t workItems(const RCParams& p, int nSrcs) {
+  return p.generic ? p.nElts : (p.nPacks + unroll_for(nSrcs) - 1) / unroll_for(nSrcs);
+}
+
+hipError_t launchBatchDt(int dt, const BatchParams& b, int op, int nSrcs, int pol, int grid, hipStream_t s) {
+  switch (dt) {
+    case 0: return launch_batch_dt0(b, op, nSrcs, pol, grid, s);
+    case 1: return launch_batch_dt1(b, op, nSrcs, pol, grid, s);
+    case 2: return launch_batch_dt2(b, op, nSrcs, pol, grid, s);
+    case 3: return launch_batch_dt3(b, op, nSrcs, pol, grid, s);
+    case 4: return launch_batch_dt4(b, op, nSrcs, pol, grid, s);
+    case 5: return launch_batch_dt5(b, op, nSrcs, pol, grid, s);
+    case 6: return launch_batch_dt6(b, op, nSrcs, pol, grid, s);
+    case 7: return launch_batch_dt7(b, op, nSrcs, pol, grid, s);
+    case 8: return launch_batch_dt8(b, op, nSrcs, pol, grid, s);
+    case 9: return launch_batch_dt9(b, op, nSrcs, pol, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// One batch launch per (nSrcs, run of <= kMaxBatch works): work i gets
+// max(1, ceil(items_i / kBlock)) workgroups (its one-shot grid), total capped at 2^24 by
+// shrinking the largest shares (the kernel grid-strides inside each work's range).
+nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int op, hipStream_t stream) {
+  if (nWorks < 0 || (nWorks > 0 && works == nullptr)) return nexrInvalidArgument;
+  for (int i = 0; i < nWorks; i++) {
+    const nexrReduceCopyWork& w = works[i];
+    nexrResult_t r = validate(w.nSrcs, w.srcs, w.nDsts, w.dsts, w.nElts, datatype, op, w.redOpArg, w.nPreOpSrcs,
+                              w.preOpArgs);
+    if (r != nexrSuccess) return r;
+  }
+  const size_t esz = typeSize(datatype);
+  const uint64_t cap = 1ull << 24;
+  for (int k = 1; k <= NEXR_MAX_SRCS; k++) {
+    BatchParams b;
+    b.nWorks = 0;
+    uint64_t blocks[kMaxBatch];
+    uint64_t streamBytes = 0;
+    auto flush = [&]() -> nexrResult_t {
+      if (b.nWorks == 0) return nexrSuccess;
+      uint64_t total = 0;
+      for (int i = 0; i < b.nWorks; i++) total += blocks[i];
+      while (total > cap) {  // rare (> 4 G packed items): halve the largest share
+        int big = 0;
+        for (int i = 1; i < b.nWorks; i++)
+          if (blocks[i] > blocks[big]) big = i;
+        uint64_t cut = blocks[big] / 2;
+        blocks[big] -= cut;
+        total -= cut;
+      }
+      b.start[0] = 0;
+      for (int i = 0; i < b.nWorks; i++) b.start[i + 1] = b.start[i] + (uint32_t)blocks[i];
+      Geometry g;
+      nexrResult_t r = pickGeometry(total, streamBytes, &g);
+      if (r != nexrSuccess) return r;
+      NEXR_HIP(launchBatchDt(datatype, b, op, k, g.pol, (int)total, stream));
+      b.nWorks = 0;
+      streamBytes = 0;
+      return nexrSuccess;
+    };
+    for (int i = 0; i < nWorks; i++) {
+      const nexrReduceCopyWork& w = works[i];
+      if (w.nSrcs != k || w.nElts == 0 || w.nDsts == 0) continue;
+      RCParams& p = b.w[b.nWorks];
+      fillParams(p, k, w.srcs, w.nDsts, w.dsts, w.nElts, esz, w.redOpArg, w.nPreOpSrcs, w.preOpArgs, nullptr,
+                 w.postOp);
+      uint64_t need = (workItems(p, k) + kBlock - 1) / kBlock;
+      blocks[b.nWorks] = need < 1 ? 1 : (need < cap ? need : cap);
+      streamBytes += (uint64_t)(k + w.nDsts) * w.nElts * esz;
+      if (++b.nWorks == kMaxBatch) {
+        nexrResult_t r = flush();
+        if (r != nexrSuccess) return r;
+      }
+    }
+    nexrResult_t r = flush();
+    if (r != nexrSuccess) return r;
+  }
+  return nexrSuccess;
+}
+
+nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                              size_t nElts, int datatype, int op, uint64_t redOpArg, int nPreOpSrcs,
+                              const uint64_t* preOpArgs, const void* prePtr, int postOp, hipStream_t stream) {
+  nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, op, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != nexrSuccess) return r;
+  if (nElts == 0 || nDsts == 0) return nexrSuccess;  // common_kernel.h:288-289: nothing to store
+  const size_t esz = typeSize(datatype);
+  RCParams p;
+  fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, nPreOpSrcs, preOpArgs, prePtr, postOp);
   Geometry g;
-  const uint64_t items = p.generic ? p.nElts : (p.nPacks + unroll_for(nSrcs) - 1) / unroll_for(nSrcs);
-  r = pickGeometry(items, (uint64_t)(nSrcs + nDsts) * nElts * esz, &g);
+  r = pickGeometry(workItems(p, nSrcs), (uint64_t)(nSrcs + nDsts) * nElts * esz, &g);
   if (r != nexrSuccess) return r;
   NEXR_HIP(launchDt(datatype, p, op, nSrcs, g, stream));
   return nexrSuccess;
@@ -242,6 +328,11 @@ NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDs
                                      nexrStream_t stream) {
   return reduceCopyDevice(nSrcs, srcs, nDsts, dsts, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs,
                           preOpArgs, nullptr, postOp, (hipStream_t)stream);
+}
+
+NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int devRedOp,
+                                          nexrStream_t stream) {
+  return reduceCopyBatch(works, nWorks, datatype, devRedOp, (hipStream_t)stream);
 }
 
 NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,

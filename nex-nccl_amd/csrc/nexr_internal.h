@@ -67,6 +67,16 @@ struct LL128Params {
 };
 hipError_t launch_ll128(int dt, const LL128Params& a, int op, int grid, hipStream_t s);
 
+// A batch of independent reduce-copies with the same (datatype, op, K) in one launch.
+constexpr int kMaxBatch = 14;  // keeps the parameter block under the 4 KiB kernel-argument limit
+struct BatchParams {
+  int nWorks;
+  uint32_t start[kMaxBatch + 1];  // work i owns workgroups [start[i], start[i+1])
+  RCParams w[kMaxBatch];
+};
+static_assert(sizeof(BatchParams) <= 4000, "batch parameters must fit the kernel-argument segment");
+static_assert(kMaxBatch == NEXR_MAX_BATCH_WORKS, "public batch limit must match the kernel's");
+
 // Launch geometry chosen by the host.
 struct Geometry {
   int grid;
@@ -81,6 +91,12 @@ NEXR_DECLARE_LAUNCH(0) NEXR_DECLARE_LAUNCH(1) NEXR_DECLARE_LAUNCH(2) NEXR_DECLAR
 NEXR_DECLARE_LAUNCH(4) NEXR_DECLARE_LAUNCH(5) NEXR_DECLARE_LAUNCH(6) NEXR_DECLARE_LAUNCH(7)
 NEXR_DECLARE_LAUNCH(8) NEXR_DECLARE_LAUNCH(9)
 #undef NEXR_DECLARE_LAUNCH
+#define NEXR_DECLARE_BATCH(dt) \
+  hipError_t launch_batch_dt##dt(const BatchParams& b, int op, int nSrcs, int pol, int grid, hipStream_t s);
+NEXR_DECLARE_BATCH(0) NEXR_DECLARE_BATCH(1) NEXR_DECLARE_BATCH(2) NEXR_DECLARE_BATCH(3)
+NEXR_DECLARE_BATCH(4) NEXR_DECLARE_BATCH(5) NEXR_DECLARE_BATCH(6) NEXR_DECLARE_BATCH(7)
+NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
+#undef NEXR_DECLARE_BATCH
 
 // Packs per lane per source in one workgroup trip (the trip covers kBlock*U packs = 16 KiB per
 // buffer). Steady-state sweeps over U in {1,2,4,8} x block in {256,512,1024} for K = 2, 4, 8

@@ -84,8 +84,10 @@ __device__ __forceinline__ void do_element(const char* const (&src)[K], char* co
     if (d < nDsts) __builtin_memcpy(dst[d] + i * esz, &out, esz);
 }
 
+// `bid`/`nblk`: this workgroup's index among the `nblk` workgroups working on `p` (the whole grid
+// for a single launch; a slice of it for a batch launch).
 template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
-__device__ __forceinline__ void body(const RCParams& p) {
+__device__ __forceinline__ void body(const RCParams& p, uint64_t bid, uint64_t nblk) {
   using T = Ty<D>;
   constexpr int esz = 16 / T::EPP;
   Fold<D, OP, K, IsMin> f(p);
@@ -103,8 +105,8 @@ __device__ __forceinline__ void body(const RCParams& p) {
 #pragma unroll
   for (int d = 0; d < NEXR_MAX_DSTS; d++) dst[d] = p.dst[d];
   const int nDsts = p.nDsts;
-  const uint64_t gid = (uint64_t)blockIdx.x * B + threadIdx.x;
-  const uint64_t nthreads = (uint64_t)gridDim.x * B;
+  const uint64_t gid = bid * B + threadIdx.x;
+  const uint64_t nthreads = nblk * B;
 
   if (p.generic) {  // pointers share no 16-B phase: every element on the scalar path
     for (uint64_t i = gid; i < p.nElts; i += nthreads) do_element<D, OP, K, IsMin>(src, dst, nDsts, f, i);
@@ -126,9 +128,9 @@ __device__ __forceinline__ void body(const RCParams& p) {
   for (int d = 0; d < NEXR_MAX_DSTS; d++) dst[d] += head * esz;
   const uint64_t nPacks = p.nPacks;
   const uint64_t nFull = nPacks / (B * U);  // groups of B*U packs
-  uint64_t g = blockIdx.x;
+  uint64_t g = bid;
   // Full groups: K*U 16-B loads in flight per lane, then the fold, then M*U stores.
-  for (; g < nFull; g += gridDim.x) {
+  for (; g < nFull; g += nblk) {
     const uint64_t off = (g * (B * U) + threadIdx.x) * 16;
     u32x4 in[U][K];
 #pragma unroll
@@ -158,14 +160,30 @@ __device__ __forceinline__ void body(const RCParams& p) {
   }
 }
 
+template <int D, int OP, int K, int POL, int U, int B>
+__device__ __forceinline__ void dispatch_minmax(const RCParams& p, uint64_t bid, uint64_t nblk) {
+  if constexpr (OP == nexrDevMinMax) {
+    if ((p.redArg & 1) == 0) body<D, OP, K, POL, true, U, B>(p, bid, nblk);  // isMin = (arg&1)==0, reduce_kernel.h:64
+    else body<D, OP, K, POL, false, U, B>(p, bid, nblk);
+  } else {
+    body<D, OP, K, POL, false, U, B>(p, bid, nblk);
+  }
+}
+
 template <int D, int OP, int K, int POL, int U = unroll_for(K), int B = kBlock>
 __global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
-  if constexpr (OP == nexrDevMinMax) {
-    if ((p.redArg & 1) == 0) body<D, OP, K, POL, true, U, B>(p);  // isMin = (arg&1)==0, reduce_kernel.h:64
-    else body<D, OP, K, POL, false, U, B>(p);
-  } else {
-    body<D, OP, K, POL, false, U, B>(p);
-  }
+  dispatch_minmax<D, OP, K, POL, U, B>(p, blockIdx.x, gridDim.x);
+}
+
+// Batch launch (the analogue of a kernel running a ncclDevWorkBatch: src/device/common.h:307-342):
+// up to kMaxBatch independent reduce-copies with the same (datatype, op, K) in one launch; work i
+// owns workgroups [start[i], start[i+1]). The work index is wave-uniform, so the descriptor is read
+// straight from the kernel-argument segment with scalar loads.
+template <int D, int OP, int K, int POL>
+__global__ __launch_bounds__(kBlock) void reduce_copy_batch_kernel(BatchParams b) {
+  int i = 0;
+  while (i + 1 < b.nWorks && blockIdx.x >= b.start[i + 1]) i++;
+  dispatch_minmax<D, OP, K, POL, unroll_for(K), kBlock>(b.w[i], blockIdx.x - b.start[i], b.start[i + 1] - b.start[i]);
 }
 
 template <int D, int OP, int K>
@@ -192,6 +210,30 @@ static hipError_t launch_op(const RCParams& p, int nSrcs, const Geometry& g, hip
   return hipErrorInvalidValue;
 }
 
+template <int D, int OP, int K>
+static hipError_t launch_batch_k(const BatchParams& b, int pol, int grid, hipStream_t s) {
+  const void* fn = pol == kPolNt       ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNt>
+                   : pol == kPolNtLoad ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNtLoad>
+                                       : (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolPlain>;
+  void* args[] = {const_cast<BatchParams*>(&b)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+}
+
+template <int D, int OP>
+static hipError_t launch_batch_op(const BatchParams& b, int nSrcs, int pol, int grid, hipStream_t s) {
+  switch (nSrcs) {
+    case 1: return launch_batch_k<D, OP, 1>(b, pol, grid, s);
+    case 2: return launch_batch_k<D, OP, 2>(b, pol, grid, s);
+    case 3: return launch_batch_k<D, OP, 3>(b, pol, grid, s);
+    case 4: return launch_batch_k<D, OP, 4>(b, pol, grid, s);
+    case 5: return launch_batch_k<D, OP, 5>(b, pol, grid, s);
+    case 6: return launch_batch_k<D, OP, 6>(b, pol, grid, s);
+    case 7: return launch_batch_k<D, OP, 7>(b, pol, grid, s);
+    case 8: return launch_batch_k<D, OP, 8>(b, pol, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 #define NEXR_CAT2(a, b) a##b
 #define NEXR_CAT(a, b) NEXR_CAT2(a, b)
 
@@ -209,4 +251,21 @@ hipError_t NEXR_CAT(launch_dt, NEXR_DT)(const RCParams& p, int op, int nSrcs, co
   return hipErrorInvalidValue;
 }
 
+}  // namespace nexr
+
+namespace nexr {
+hipError_t NEXR_CAT(launch_batch_dt, NEXR_DT)(const BatchParams& b, int op, int nSrcs, int pol, int grid,
+                                              hipStream_t s) {
+  constexpr int D = NEXR_DT;
+  switch (op) {
+    case nexrDevSum: return launch_batch_op<D, nexrDevSum>(b, nSrcs, pol, grid, s);
+    case nexrDevProd: return launch_batch_op<D, nexrDevProd>(b, nSrcs, pol, grid, s);
+    case nexrDevMinMax: return launch_batch_op<D, nexrDevMinMax>(b, nSrcs, pol, grid, s);
+    case nexrDevPreMulSum: return launch_batch_op<D, nexrDevPreMulSum>(b, nSrcs, pol, grid, s);
+    case nexrDevSumPostDiv:
+      if constexpr (Ty<D>::kIsInt) return launch_batch_op<D, nexrDevSumPostDiv>(b, nSrcs, pol, grid, s);
+      break;
+  }
+  return hipErrorInvalidValue;
+}
 }  // namespace nexr

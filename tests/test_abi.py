@@ -96,6 +96,39 @@ def test_empty_calls_are_noops(nexr):
     assert _call(nexr, ndsts=0) == 0
 
 
+def test_batch_work_layout_matches_header(nexr):
+    # nexrReduceCopyWork: int, int, 8 src ptrs, 8 dst ptrs, size_t, u64, int, int, 8 u64.
+    W = nexr.ReduceCopyWork
+    assert ctypes.sizeof(W) == 8 + 64 + 64 + 8 + 8 + 8 + 64
+    assert (W.srcs.offset, W.dsts.offset, W.nElts.offset, W.preOpArgs.offset) == (8, 72, 136, 160)
+    assert re.search(r"#define\s+NEXR_MAX_BATCH_WORKS\s+(\d+)", open(HEADER).read()).group(1) == str(
+        nexr.MAX_BATCH_WORKS)
+
+
+def test_batch_validates_every_work_before_launching(nexr):
+    L = nexr.lib()
+    good = nexr.make_work([0x1000, 0x2000], [0x3000], 16)
+    bad_null = nexr.make_work([0x1000, 0], [0x3000], 16)
+    bad_pre = nexr.make_work([0x1000], [0x3000], 16, pre_op_args=[1])
+    bad_pre.nPreOpSrcs = 2  # > nSrcs
+    for bad in (bad_null, bad_pre):
+        arr = (nexr.ReduceCopyWork * 3)(good, bad, good)
+        assert L.nexrReduceCopyBatch(arr, 3, 7, 0, None) == 4
+    arr = (nexr.ReduceCopyWork * 1)(good)
+    assert L.nexrReduceCopyBatch(arr, 1, 10, 0, None) == 4  # fp8
+    assert L.nexrReduceCopyBatch(arr, 1, 7, 4, None) == 4   # SumPostDiv on a float
+    assert L.nexrReduceCopyBatch(arr, -1, 7, 0, None) == 4
+    assert L.nexrReduceCopyBatch(None, 2, 7, 0, None) == 4
+    # Empty batches and works with nothing to store never reach the device.
+    assert L.nexrReduceCopyBatch(None, 0, 7, 0, None) == 0
+    empty = nexr.make_work([0x1000, 0x2000], [0x3000], 0)
+    nodst = nexr.make_work([0x1000, 0x2000], [], 16)
+    arr = (nexr.ReduceCopyWork * 2)(empty, nodst)
+    assert L.nexrReduceCopyBatch(arr, 2, 7, 0, None) == 0
+    with pytest.raises(nexr.NexrError):
+        nexr.make_work([1] * 9, [2], 4)
+
+
 @pytest.mark.parametrize("dt", sorted(mg.DT_NAMES) + [10, 11])
 @pytest.mark.parametrize("op,nranks", [(0, 2), (1, 2), (2, 4), (3, 4), (4, 1), (4, 3), (4, 8), (5, 2)])
 def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):

@@ -1,0 +1,141 @@
+"""GPU parity tests of nexrReduceCopyBatch: every work of a batch against the oracle, bit-exact.
+
+A batch carries many independent reduce-copies of one (datatype, op) — the analogue of one kernel
+launch running a ncclDevWorkBatch (src/device/common.h:165-200) — so the cases mix K, M, sizes,
+pointer phases and per-work op arguments (min next to max, different PreMulSum scalars and
+divisors) inside one call, with more works than fit one launch, and check guard bytes around every
+destination.
+"""
+import numpy as np
+import pytest
+
+import make_golden as mg
+from test_reduce_copy_gpu import OPS, _case_args, _to_dev, same
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+class _Work:
+    def __init__(self, nexr, oracle, dt, op, name, k, m, n, seed, rng, offsets="random", in_place=False):
+        esz = np.dtype(mg.STORE[dt]).itemsize
+        if offsets == "zero":
+            so, do = [0] * k, [0] * m
+        elif offsets == "phase":
+            ph = int(rng.integers(0, 16 // esz)) * esz
+            so, do = [ph] * k, [ph] * m
+        else:
+            so = [int(rng.integers(0, 16)) for _ in range(k)]
+            do = [int(rng.integers(0, 16)) for _ in range(m)]
+        self.dt, self.n, self.esz, self.do = dt, n, esz, do
+        self.arg, self.pre, self.post = _case_args(dt, name, op, k, rng)
+        self.srcs = mg.gen_inputs(dt, k, max(n, 1), seed, special=True)
+        if n == 0:
+            self.srcs = [s[:0] for s in self.srcs]
+        self.exp = oracle.reduce_copy(self.srcs, 1, dt, op, self.arg, self.pre, self.post)[0] if n else None
+        self.sbufs = [_to_dev(s, o) for s, o in zip(self.srcs, so)]
+        sptrs = [b.data_ptr() + o for b, o in zip(self.sbufs, so)]
+        if in_place:
+            self.dbufs, do = [self.sbufs[0]], [so[0]]
+            self.do = do
+            self.guard = False
+        else:
+            self.dbufs = [torch.full((n * esz + o + 64,), 0x5A, dtype=torch.uint8, device="cuda") for o in do]
+            self.guard = True
+        dptrs = [b.data_ptr() + o for b, o in zip(self.dbufs, do)]
+        self.work = nexr.make_work(sptrs, dptrs, n, self.arg, self.pre, self.post)
+
+    def check(self, tag):
+        if self.n == 0:
+            for b in self.dbufs:
+                if self.guard:
+                    assert (b.cpu().numpy() == 0x5A).all(), (tag, "empty work wrote")
+            return
+        for b, o in zip(self.dbufs, self.do):
+            host = b.cpu().numpy()
+            nb = self.n * self.esz
+            if self.guard:
+                assert (host[:o] == 0x5A).all() and (host[o + nb:] == 0x5A).all(), (tag, "write outside dst")
+            got = host[o:o + nb].view(mg.STORE[self.dt])
+            assert same(self.dt, got, self.exp), tag
+
+
+SIZES = [0, 1, 2, 7, 15, 16, 17, 255, 1023, 4097, 65535, 300_001]
+
+
+@pytest.mark.parametrize("dt", sorted(mg.DT_NAMES))
+def test_batch_mixed_works_match_oracle(nexr, oracle, dt, dev):
+    rng = np.random.default_rng(100 + dt)
+    for name, op in OPS:
+        if name == "sumpostdiv" and dt not in mg.INTS:
+            continue
+        n_works = int(rng.choice([1, 5, 14, 15, 37]))
+        works = []
+        for w in range(n_works):
+            k = int(rng.integers(1, 9))
+            m = int(rng.integers(1, 5))
+            n = int(rng.choice(SIZES))
+            mode = ["zero", "phase", "random"][int(rng.integers(0, 3))]
+            works.append(_Work(nexr, oracle, dt, op, name, k, m, n, 9000 + 97 * w + op, rng, mode))
+        nexr.reduce_copy_batch([w.work for w in works], dt, op, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for i, w in enumerate(works):
+            w.check((mg.DT_NAMES[dt], name, i, w.n))
+
+
+def test_batch_min_and_max_in_one_launch(nexr, oracle, dev):
+    # MinMax carries min/max in each work's redOpArg (reduce_kernel.h:64), so one launch mixes them.
+    rng = np.random.default_rng(7)
+    for dt in (mg.I8, mg.U32, mg.F16, mg.F64):
+        works = []
+        for w in range(14):
+            works.append(_Work(nexr, oracle, dt, mg.MINMAX, "max" if w % 2 else "min", 3, 1, 20_000 + w, 40 + w, rng))
+        nexr.reduce_copy_batch([w.work for w in works], dt, mg.MINMAX)
+        torch.cuda.synchronize()
+        for i, w in enumerate(works):
+            w.check((mg.DT_NAMES[dt], i))
+
+
+def test_batch_in_place_and_large_works(nexr, oracle, dev):
+    # Large works (tens of MiB) beside tiny ones: each gets its proportional workgroup range.
+    rng = np.random.default_rng(11)
+    works = [
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 2, 1, 8_000_003, 1, rng, "zero"),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 2, 2, 3, 2, rng, "random"),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 4, 1, 5_000_001, 3, rng, "phase", in_place=True),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 2, 1, 1, 4, rng, "zero", in_place=True),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 8, 3, 1_000_000, 5, rng, "random"),
+    ]
+    s = torch.cuda.Stream()
+    nexr.reduce_copy_batch([w.work for w in works], mg.F32, mg.SUM, s.cuda_stream)
+    s.synchronize()
+    for i, w in enumerate(works):
+        w.check(("large", i))
+
+
+def test_batch_equals_separate_calls_bitwise(nexr, dev):
+    # The same works through nexrReduceCopy one by one and through one batch give identical bytes.
+    g = torch.Generator(device="cuda").manual_seed(3)
+    srcs = [torch.randn(1 << 16, device="cuda", generator=g, dtype=torch.bfloat16) for _ in range(8)]
+    works, outs_b, outs_s = [], [], []
+    for i in range(1, 9):
+        n = 1000 * i + i
+        ob = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+        os_ = torch.empty_like(ob)
+        ptrs = [t.data_ptr() + 2 * i for t in srcs[:i]]
+        works.append(nexr.make_work(ptrs, [ob.data_ptr()], n))
+        nexr.reduce_copy_ptrs(ptrs, [os_.data_ptr()], n, nexr.DataType.Bfloat16, nexr.DevRedOp.Sum,
+                              stream=torch.cuda.current_stream().cuda_stream)
+        outs_b.append(ob)
+        outs_s.append(os_)
+    nexr.reduce_copy_batch(works, nexr.DataType.Bfloat16, nexr.DevRedOp.Sum, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for a, b in zip(outs_b, outs_s):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
