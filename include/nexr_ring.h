@@ -78,6 +78,35 @@ NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t comm, const void* const* 
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t comm);
 
+/*
+ * Process ranks over peer memory (the §8(f) xGMI ring step): one process per GPU, each process one
+ * rank of the same ring schedule. Like the reference's P2P transport in write mode
+ * (src/transport/p2p.cc:231-240, :299, :402, :514-515, :542-543): every rank allocates the FIFO it
+ * receives into, exports it with hipIpcGetMemHandle, and maps the next rank's FIFO with
+ * hipIpcOpenMemHandle; its reduce-copy kernels write straight into that peer FIFO (over xGMI when
+ * the ranks drive different GPUs). Step counters and the rendezvous live in a POSIX shared-memory
+ * segment `shmName` (single node): every rank passes the same fresh name ("/name", no other '/');
+ * the last rank to destroy its communicator unlinks it. Create blocks until all nRanks joined
+ * (bounded by timeoutMs). Every rank must then issue the same sequence of nexrPeerRingAllReduce
+ * calls (same count, datatype, op). Buffers are device memory on `device`. Destroy with
+ * nexrRingCommDestroy.
+ */
+typedef struct {
+  int nRanks;
+  int rank;
+  int device;          /* HIP device of this rank's buffers and kernels */
+  size_t buffBytes;    /* 0 = the protocol default (as nexrRingConfig) */
+  int protocol;        /* nexrRingProto_t */
+  int timeoutMs;       /* rendezvous and per-wait bound; 0 = 60000 */
+  const char* shmName; /* shared by all ranks of this communicator */
+} nexrPeerRingConfig;
+
+NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* comm, const nexrPeerRingConfig* config);
+
+/* ncclAllReduce for this process's rank (sendbuff/recvbuff on config->device; in-place allowed). */
+NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
+                                            int datatype, int op);
+
 #ifdef __cplusplus
 }
 #endif

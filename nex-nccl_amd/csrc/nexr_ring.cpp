@@ -4,8 +4,12 @@
 // configs[0] ("fp32 sum all-reduce, 4 MiB, 2 CPU-emulated ranks"): the schedule is unchanged,
 // only the primitive underneath is the MI355X kernel.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -27,11 +31,35 @@ constexpr size_t kDefaultLL128BuffBytes = 120 * 640 * kSteps * 8;  // DEFAULT_LL
 
 // One directed connection prev -> r. The FIFO belongs to the receiver (the sender writes into it,
 // like a P2P/SHM transport's recv buffer, src/include/device.h:753-771).
-struct Conn {
-  char* fifo = nullptr;
+struct ConnState {
   alignas(64) std::atomic<uint64_t> tail{0};  // steps published by the sender   (postPeer, Send)
   alignas(64) std::atomic<uint64_t> head{0};  // steps released by the receiver  (postPeer, Recv)
 };
+struct Conn {
+  char* fifo = nullptr;
+  ConnState own;
+  ConnState* st = &own;  // the counters: `own` for thread ranks, a shared-memory slot for process ranks
+};
+
+// Process ranks (nexrPeerRingCommCreate): one POSIX shared-memory segment per communicator holds
+// the rendezvous, every connection's head/tail counters and a common abort word. Slot r belongs to
+// rank r: its FIFO's IPC handle and the counters of the connection INTO rank r.
+constexpr uint32_t kPeerMagic = 0x6e657872u;  // "nexr"
+struct PeerHeader {
+  std::atomic<uint32_t> initState;  // 0 fresh, 1 being configured, 2 configured
+  std::atomic<uint32_t> joined;
+  std::atomic<uint32_t> left;
+  std::atomic<uint32_t> abort;
+  uint32_t magic, nRanks, protocol, pad;
+  uint64_t buffBytes;
+};
+struct PeerSlot {
+  hipIpcMemHandle_t fifoHandle;
+  alignas(64) ConnState conn;
+};
+size_t peerShmBytes(int n) { return sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot); }
+PeerHeader* peerHeader(void* base) { return (PeerHeader*)base; }
+PeerSlot* peerSlot(void* base, int r) { return (PeerSlot*)((char*)base + sizeof(PeerHeader)) + r; }
 
 int64_t divUp(int64_t a, int64_t b) { return (a + b - 1) / b; }
 int64_t alignUp(int64_t a, int64_t b) { return divUp(a, b) * b; }
@@ -51,6 +79,14 @@ struct nexrRingComm {
   int proto = nexrRingProtoSimple;
   bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
   bool broken = false;
+  // Process ranks: this process is rank `self` only.
+  bool peer = false;
+  int self = 0;
+  void* shm = nullptr;
+  size_t shmBytes = 0;
+  char shmName[256] = {0};
+  char* peerFifo = nullptr;  // the next rank's FIFO, IPC-mapped into this process
+  bool peerFifoIpc = false;
 };
 
 namespace {
@@ -58,10 +94,15 @@ namespace {
 struct Shared {
   std::atomic<bool> abort{false};
   std::atomic<int> firstError{0};
+  std::atomic<uint32_t>* remoteAbort = nullptr;  // process ranks: the communicator-wide abort word
   void fail(nexrResult_t r) {
     int expected = 0;
     firstError.compare_exchange_strong(expected, (int)r);
     abort.store(true);
+    if (remoteAbort) remoteAbort->store(1, std::memory_order_release);
+  }
+  bool aborted() const {
+    return abort.load(std::memory_order_relaxed) || (remoteAbort && remoteAbort->load(std::memory_order_acquire));
   }
 };
 
@@ -93,7 +134,10 @@ struct Prims {
     auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 0;; spins++) {
       if (a.load(std::memory_order_acquire) >= target) return true;
-      if (sh->abort.load(std::memory_order_relaxed)) return false;
+      if (sh->aborted()) {
+        sh->fail(nexrRemoteError);
+        return false;
+      }
       if ((spins & 1023) == 0 &&
           std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) {
         sh->fail(nexrInternalError);
@@ -119,11 +163,11 @@ struct Prims {
       const char* recvPtr = nullptr;
       char* sendPtr = nullptr;
       if (Recv) {  // wait for the peer's data: tail >= step + StepPerSlice
-        if (!waitAtLeast(recvConn->tail, rs + kSliceSteps)) return false;
+        if (!waitAtLeast(recvConn->st->tail, rs + kSliceSteps)) return false;
         recvPtr = recvConn->fifo + (rs % kSteps) * c->stepBytes;
       }
       if (Send) {  // wait for credit: head + NCCL_STEPS >= step + StepPerSlice
-        if (ss + kSliceSteps > (uint64_t)kSteps && !waitAtLeast(sendConn->head, ss + kSliceSteps - kSteps))
+        if (ss + kSliceSteps > (uint64_t)kSteps && !waitAtLeast(sendConn->st->head, ss + kSliceSteps - kSteps))
           return false;
         sendPtr = sendConn->fifo + (ss % kSteps) * c->stepBytes;
       }
@@ -153,11 +197,11 @@ struct Prims {
       // postPeer (prims_simple.h:177-188): release the slot / publish the data.
       if (Recv) {
         rs += kSliceSteps;
-        recvConn->head.store(rs, std::memory_order_release);
+        recvConn->st->head.store(rs, std::memory_order_release);
       }
       if (Send) {
         ss += kSliceSteps;
-        sendConn->tail.store(ss, std::memory_order_release);
+        sendConn->st->tail.store(ss, std::memory_order_release);
       }
       offset += sliceSize;
     }
@@ -173,8 +217,8 @@ struct Prims {
     nelem = nelem < 0 ? 0 : nelem;
     uint64_t& rs = c->recvStep[rank];
     uint64_t& ss = c->sendStep[rank];
-    if (Send && ss + 1 > (uint64_t)kSteps && !waitAtLeast(sendConn->head, ss + 1 - kSteps)) return false;
-    if (Recv && !waitAtLeast(recvConn->tail, rs + 1)) return false;
+    if (Send && ss + 1 > (uint64_t)kSteps && !waitAtLeast(sendConn->st->head, ss + 1 - kSteps)) return false;
+    if (Recv && !waitAtLeast(recvConn->st->tail, rs + 1)) return false;
     if (nelem > 0) {
       const void* recvLines[1] = {recvConn->fifo + (rs % kSteps) * c->stepBytes};
       void* sendLines[1] = {sendConn->fifo + (ss % kSteps) * c->stepBytes};
@@ -202,11 +246,11 @@ struct Prims {
     }
     if (Recv) {  // postRecv (:80-83)
       rs += 1;
-      recvConn->head.store(rs, std::memory_order_release);
+      recvConn->st->head.store(rs, std::memory_order_release);
     }
     if (Send) {  // incSend (:85-93); the flag-wrap cleanup at NCCL_LL_CLEAN_MASK needs ~2^31 steps
       ss += 1;
-      sendConn->tail.store(ss, std::memory_order_release);
+      sendConn->st->tail.store(ss, std::memory_order_release);
     }
     return true;
   }
@@ -287,6 +331,56 @@ nexrResult_t defaultLL128Fn(const void* src, int srcIsInput, int nRecv, const vo
 nexrResult_t defaultDeviceFn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t n, int dt,
                              int op, uint64_t arg, int nPre, const uint64_t* pre, int post, nexrStream_t s) {
   return nexrReduceCopy(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
+}
+
+Prims makePrims(nexrRingComm* c, Shared* sh, int rank, Conn* recvConn, Conn* sendConn, const void* sendbuff,
+                void* recvbuff, size_t esz, int datatype, const nexrDevRedOpFull& red, bool device) {
+  Prims p;
+  p.c = c;
+  p.sh = sh;
+  p.rank = rank;
+  p.recvConn = recvConn;
+  p.sendConn = sendConn;
+  p.userInput = (const char*)sendbuff;
+  p.userOutput = (char*)recvbuff;
+  p.esz = esz;
+  p.stepSize = (int64_t)(c->stepBytes / esz);
+  p.datatype = datatype;
+  p.devOp = red.op;
+  p.redOpArgs[0] = red.scalarArg;
+  p.fn = c->cfg.fn;
+  p.llFn = c->cfg.llFn;
+  p.ll128Fn = c->cfg.ll128Fn;
+  p.status = c->status[rank];
+  p.stream = c->streams[rank];
+  p.device = device;
+  return p;
+}
+
+// ncclLaunchOneRank (onerank.cc:48-83) for rank `r`'s buffers.
+nexrResult_t oneRank(nexrRingComm* c, int r, const void* sendbuff, void* recvbuff, size_t count, int datatype,
+                     const nexrDevRedOpFull& red, size_t esz) {
+  const bool device = c->cfg.memMode == nexrRingDeviceMemory;
+  if (device) (void)hipSetDevice(c->devices[r]);
+  if (red.op == nexrDevPreMulSum) {
+    uint64_t arg = red.scalarArg;
+    const void* srcs[1] = {sendbuff};
+    void* dsts[1] = {recvbuff};
+    nexrResult_t res = c->cfg.fn(1, srcs, 1, dsts, count, datatype, nexrDevPreMulSum, arg, 1, &arg, 1,
+                                 (nexrStream_t)c->streams[r]);
+    if (res == nexrSuccess && device && hipStreamSynchronize(c->streams[r]) != hipSuccess)
+      res = nexrUnhandledCudaError;
+    return res;
+  }
+  if (sendbuff != recvbuff) {
+    if (device) {
+      if (hipMemcpy(recvbuff, sendbuff, count * esz, hipMemcpyDeviceToDevice) != hipSuccess)
+        return nexrUnhandledCudaError;
+    } else {
+      memcpy(recvbuff, sendbuff, count * esz);
+    }
+  }
+  return nexrSuccess;
 }
 
 }  // namespace
@@ -403,50 +497,15 @@ NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sen
   if (count == 0) return nexrSuccess;
   const bool device = c->cfg.memMode == nexrRingDeviceMemory;
 
-  if (n == 1) {  // ncclLaunchOneRank (onerank.cc:48-83)
-    if (device) (void)hipSetDevice(c->devices[0]);
-    if (red.op == nexrDevPreMulSum) {
-      uint64_t arg = red.scalarArg;
-      r = c->cfg.fn(1, sendbuffs, 1, recvbuffs, count, datatype, nexrDevPreMulSum, arg, 1, &arg, 1,
-                    (nexrStream_t)c->streams[0]);
-      if (r == nexrSuccess && device && hipStreamSynchronize(c->streams[0]) != hipSuccess) r = nexrUnhandledCudaError;
-      return r;
-    }
-    if (sendbuffs[0] != recvbuffs[0]) {
-      if (device) {
-        if (hipMemcpy(recvbuffs[0], sendbuffs[0], count * esz, hipMemcpyDeviceToDevice) != hipSuccess)
-          return nexrUnhandledCudaError;
-      } else {
-        memcpy(recvbuffs[0], sendbuffs[0], count * esz);
-      }
-    }
-    return nexrSuccess;
-  }
+  if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
 
   Shared sh;
   std::vector<std::thread> threads;
   for (int rank = 0; rank < n; rank++) {
     threads.emplace_back([&, rank] {
       if (device || c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-      Prims p;
-      p.c = c;
-      p.sh = &sh;
-      p.rank = rank;
-      p.recvConn = c->conns[rank];
-      p.sendConn = c->conns[(rank + 1) % n];
-      p.userInput = (const char*)sendbuffs[rank];
-      p.userOutput = (char*)recvbuffs[rank];
-      p.esz = esz;
-      p.stepSize = (int64_t)(c->stepBytes / esz);
-      p.datatype = datatype;
-      p.devOp = red.op;
-      p.redOpArgs[0] = red.scalarArg;
-      p.fn = c->cfg.fn;
-      p.llFn = c->cfg.llFn;
-      p.ll128Fn = c->cfg.ll128Fn;
-      p.status = c->status[rank];
-      p.stream = c->streams[rank];
-      p.device = device;
+      Prims p = makePrims(c, &sh, rank, c->conns[rank], c->conns[(rank + 1) % n], sendbuffs[rank], recvbuffs[rank],
+                          esz, datatype, red, device);
       runRing(p, n, (int64_t)count);
     });
   }
@@ -460,6 +519,20 @@ NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sen
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
   if (!c) return nexrInvalidArgument;
+  if (c->peer) {
+    if (!c->streams.empty() && c->streams[c->self]) (void)hipStreamSynchronize(c->streams[c->self]);
+    if (c->peerFifoIpc && c->peerFifo) (void)hipIpcCloseMemHandle(c->peerFifo);
+    if (c->shm) {
+      PeerHeader* h = peerHeader(c->shm);
+      // The last rank to leave removes the segment's name (each rank still unmaps its own view).
+      if (h->joined.load() > 0 && h->left.fetch_add(1) + 1 == h->nRanks) shm_unlink(c->shmName);
+      munmap(c->shm, c->shmBytes);
+    }
+    for (size_t r = 0; r < c->conns.size(); r++) {
+      c->conns[r]->st = &c->conns[r]->own;           // counters lived in the unmapped segment
+      if ((int)r != c->self) c->conns[r]->fifo = nullptr;  // only this rank's FIFO is owned here
+    }
+  }
   for (size_t r = 0; r < c->conns.size(); r++) {
     Conn* k = c->conns[r];
     if (k->fifo) {
@@ -483,6 +556,154 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
       (void)hipStreamDestroy(c->streams[r]);
     }
   delete c;
+  return nexrSuccess;
+}
+
+// ---- process ranks: one process per GPU, FIFOs shared over IPC (xGMI between GPUs) ----------------
+// The reference's P2P transport in write mode: the receiver allocates its FIFO and exports it
+// (src/transport/p2p.cc:231-240), the sender maps it with cudaIpcOpenMemHandle(…LazyEnablePeerAccess)
+// (:299) and its reduce-copy writes straight into it (NCCL_P2P_WRITE, :402); send/recv head and
+// tail counters pair up as in p2pSendConnect/p2pRecvConnect (:514-515, :542-543). Here the steps are
+// driven by each rank's host thread, so the counters live in host shared memory.
+NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeerRingConfig* cfg) {
+  if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024 || cfg->rank < 0 || cfg->rank >= cfg->nRanks)
+    return nexrInvalidArgument;
+  if (!cfg->shmName || cfg->shmName[0] != '/' || strlen(cfg->shmName) >= 255 || strchr(cfg->shmName + 1, '/'))
+    return nexrInvalidArgument;
+  if (cfg->protocol != nexrRingProtoSimple && cfg->protocol != nexrRingProtoLL && cfg->protocol != nexrRingProtoLL128)
+    return nexrInvalidArgument;
+  nexrRingConfig rc;
+  memset(&rc, 0, sizeof(rc));
+  rc.nRanks = cfg->nRanks;
+  rc.buffBytes = cfg->buffBytes;
+  rc.memMode = nexrRingDeviceMemory;
+  rc.timeoutMs = cfg->timeoutMs;
+  rc.protocol = cfg->protocol;
+  auto* c = new nexrRingComm();
+  c->cfg = rc;
+  c->proto = cfg->protocol;
+  c->ll = cfg->protocol != nexrRingProtoSimple;
+  if (c->cfg.buffBytes == 0)
+    c->cfg.buffBytes = c->proto == nexrRingProtoLL ? kDefaultLLBuffBytes
+                       : c->proto == nexrRingProtoLL128 ? kDefaultLL128BuffBytes : kDefaultBuffBytes;
+  if (c->cfg.buffBytes % (kSteps * 16) != 0 || (c->proto == nexrRingProtoLL128 && c->cfg.buffBytes % (kSteps * 2048) != 0)) {
+    delete c;
+    return nexrInvalidArgument;
+  }
+  c->cfg.fn = defaultDeviceFn;
+  c->cfg.llFn = defaultLLFn;
+  c->cfg.ll128Fn = defaultLL128Fn;
+  c->stepBytes = c->cfg.buffBytes / kSteps;
+  c->peer = true;
+  const int n = cfg->nRanks, me = cfg->rank, next = (me + 1) % n;
+  c->self = me;
+  c->recvStep.assign(n, 0);
+  c->sendStep.assign(n, 0);
+  c->devices.assign(n, cfg->device);
+  c->streams.assign(n, nullptr);
+  c->status.assign(n, nullptr);
+  c->pinnedStatus = true;
+  for (int r = 0; r < n; r++) c->conns.push_back(new Conn());
+  strncpy(c->shmName, cfg->shmName, sizeof(c->shmName) - 1);
+  auto fail = [&](nexrResult_t r) {
+    if (c->shm) peerHeader(c->shm)->abort.store(1);
+    nexrRingCommDestroy(c);
+    return r;
+  };
+  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreate(&c->streams[me]) != hipSuccess)
+    return fail(nexrUnhandledCudaError);
+  if (c->ll) {
+    if (hipHostMalloc((void**)&c->status[me], sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+      return fail(nexrUnhandledCudaError);
+    *c->status[me] = 0;
+  }
+  // The FIFO into this rank. Uncached device memory: it is written by another process's kernels
+  // (over xGMI when that process drives another GPU) between this rank's launches.
+  // NEXR_PEER_FIFO_UNCACHED=0 selects ordinary (coarse-grained) device memory instead.
+  const char* unc = getenv("NEXR_PEER_FIFO_UNCACHED");
+  const bool uncached = !(unc && unc[0] == '0');
+  if ((uncached ? hipExtMallocWithFlags((void**)&c->conns[me]->fifo, c->cfg.buffBytes, hipDeviceMallocUncached)
+                : hipMalloc((void**)&c->conns[me]->fifo, c->cfg.buffBytes)) != hipSuccess)
+    return fail(nexrUnhandledCudaError);
+  // Rendezvous segment.
+  c->shmBytes = peerShmBytes(n);
+  int fd = shm_open(c->shmName, O_CREAT | O_RDWR, 0600);
+  if (fd < 0) return fail(nexrSystemError);
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || (sb.st_size != 0 && (size_t)sb.st_size != c->shmBytes) ||
+      (sb.st_size == 0 && ftruncate(fd, (off_t)c->shmBytes) != 0)) {
+    close(fd);
+    return fail(sb.st_size != 0 ? nexrInvalidUsage : nexrSystemError);
+  }
+  c->shm = mmap(nullptr, c->shmBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (c->shm == MAP_FAILED) {
+    c->shm = nullptr;
+    return fail(nexrSystemError);
+  }
+  PeerHeader* h = peerHeader(c->shm);
+  const int timeoutMs = cfg->timeoutMs > 0 ? cfg->timeoutMs : 60000;
+  auto waitFor = [&](auto pred) {
+    auto t0 = std::chrono::steady_clock::now();
+    while (!pred()) {
+      if (h->abort.load(std::memory_order_acquire)) return false;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    return true;
+  };
+  uint32_t fresh = 0;
+  if (h->initState.compare_exchange_strong(fresh, 1)) {
+    h->magic = kPeerMagic;
+    h->nRanks = (uint32_t)n;
+    h->protocol = (uint32_t)c->proto;
+    h->buffBytes = c->cfg.buffBytes;
+    h->initState.store(2, std::memory_order_release);
+  } else if (!waitFor([&] { return h->initState.load(std::memory_order_acquire) == 2; })) {
+    return fail(nexrRemoteError);
+  }
+  if (h->magic != kPeerMagic || h->nRanks != (uint32_t)n || h->protocol != (uint32_t)c->proto ||
+      h->buffBytes != c->cfg.buffBytes)
+    return fail(nexrInvalidUsage);  // ranks disagree on the communicator (or a stale segment)
+  PeerSlot* mine = peerSlot(c->shm, me);
+  if (hipIpcGetMemHandle(&mine->fifoHandle, c->conns[me]->fifo) != hipSuccess) return fail(nexrUnhandledCudaError);
+  c->conns[me]->st = &mine->conn;
+  h->joined.fetch_add(1, std::memory_order_acq_rel);  // publishes the handle
+  if (!waitFor([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t)n; })) return fail(nexrRemoteError);
+  if (next != me) {
+    hipIpcMemHandle_t hd = peerSlot(c->shm, next)->fifoHandle;
+    if (hipIpcOpenMemHandle((void**)&c->peerFifo, hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+      return fail(nexrUnhandledCudaError);
+    c->peerFifoIpc = true;
+    c->conns[next]->fifo = c->peerFifo;
+    c->conns[next]->st = &peerSlot(c->shm, next)->conn;
+  }
+  *out = c;
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
+                                            int datatype, int op) {
+  if (!c || !c->peer) return nexrInvalidArgument;
+  if (c->broken) return nexrInvalidUsage;
+  const int n = c->cfg.nRanks, me = c->self;
+  const size_t esz = nexrTypeSize(datatype);
+  if (esz == 0 || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
+  nexrDevRedOpFull red;
+  nexrResult_t r = nexrHostToDevRedOp(&red, op, datatype, n);
+  if (r != nexrSuccess) return r;
+  if (count > 0 && (!sendbuff || !recvbuff)) return nexrInvalidArgument;
+  if (count == 0) return nexrSuccess;
+  (void)hipSetDevice(c->devices[me]);
+  if (n == 1) return oneRank(c, me, sendbuff, recvbuff, count, datatype, red, esz);
+  Shared sh;
+  sh.remoteAbort = &peerHeader(c->shm)->abort;
+  Prims p = makePrims(c, &sh, me, c->conns[me], c->conns[(me + 1) % n], sendbuff, recvbuff, esz, datatype, red, true);
+  runRing(p, n, (int64_t)count);
+  if (sh.firstError.load() != 0) {
+    c->broken = true;
+    return (nexrResult_t)sh.firstError.load();
+  }
   return nexrSuccess;
 }
 

@@ -14,7 +14,8 @@ from . import NexrError, Result, _check, lib
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 RING_LIB_PATH = os.path.join(_HERE, "libnexr_ring.so")
-RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingCommDestroy")
+RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
+                    "nexrPeerRingAllReduce")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -34,6 +35,12 @@ class RingConfig(ctypes.Structure):
                 ("llFn", ctypes.c_void_p), ("ll128Fn", ctypes.c_void_p)]
 
 
+class PeerRingConfig(ctypes.Structure):
+    _fields_ = [("nRanks", ctypes.c_int), ("rank", ctypes.c_int), ("device", ctypes.c_int),
+                ("buffBytes", ctypes.c_size_t), ("protocol", ctypes.c_int), ("timeoutMs", ctypes.c_int),
+                ("shmName", ctypes.c_char_p)]
+
+
 _ring = None
 
 
@@ -49,6 +56,11 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         L.nexrRingAllReduce.restype = ctypes.c_int
+        L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
+        L.nexrPeerRingCommCreate.restype = ctypes.c_int
+        L.nexrPeerRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_int, ctypes.c_int]
+        L.nexrPeerRingAllReduce.restype = ctypes.c_int
         L.nexrRingCommDestroy.argtypes = [ctypes.c_void_p]
         L.nexrRingCommDestroy.restype = ctypes.c_int
         _ring = L
@@ -75,6 +87,43 @@ class RingComm:
         s = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in sendbuffs])
         r = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in recvbuffs])
         _check(ring_lib().nexrRingAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrRingAllReduce")
+
+    def close(self) -> None:
+        if self._h:
+            ring_lib().nexrRingCommDestroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PeerRingComm:
+    """This process's rank of a ring whose ranks are processes (one per GPU), FIFOs shared over IPC.
+
+    Every rank passes the same fresh ``shm_name`` (e.g. made by rank 0 and broadcast out of band);
+    the constructor blocks until all ``n_ranks`` processes have joined."""
+
+    def __init__(self, n_ranks: int, rank: int, shm_name: str, device: int = 0, buff_bytes: int = 0,
+                 protocol: int = PROTO_SIMPLE, timeout_ms: int = 0):
+        self._name = shm_name.encode()
+        cfg = PeerRingConfig(n_ranks, rank, device, buff_bytes, protocol, timeout_ms, self._name)
+        h = ctypes.c_void_p()
+        _check(ring_lib().nexrPeerRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrPeerRingCommCreate")
+        self._h = h
+        self.n_ranks, self.rank = n_ranks, rank
+
+    def all_reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int) -> None:
+        _check(ring_lib().nexrPeerRingAllReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
+                                                int(datatype), int(op)), "nexrPeerRingAllReduce")
 
     def close(self) -> None:
         if self._h:

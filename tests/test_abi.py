@@ -169,3 +169,18 @@ def test_package_fails_loudly_without_library(nexr, monkeypatch, tmp_path):
     monkeypatch.setattr(nexr, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(nexr.NexrError):
         nexr.lib()
+
+
+def test_peer_ring_rejects_bad_configs_before_the_device():
+    import importlib
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    L = ring.ring_lib()
+    h = ctypes.c_void_p()
+    cases = [dict(nRanks=0), dict(rank=2), dict(rank=-1), dict(shmName=b"noslash"), dict(shmName=b"/a/b"),
+             dict(shmName=None), dict(protocol=3), dict(buffBytes=1000), dict(protocol=2, buffBytes=8 * 16 * 100)]
+    for bad in cases:
+        f = dict(nRanks=2, rank=0, device=0, buffBytes=0, protocol=0, timeoutMs=10, shmName=b"/nexr_abi_test")
+        f.update(bad)
+        cfg = ring.PeerRingConfig(**f)
+        assert L.nexrPeerRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)) == 4, bad
+    assert L.nexrPeerRingAllReduce(None, None, None, 0, 7, 0) == 4

@@ -1,0 +1,86 @@
+"""GPU tests of the process-per-rank peer ring (§8(f) #4): each rank is its own process, FIFOs are
+shared over IPC (hipIpcGetMemHandle / hipIpcOpenMemHandle) and every reduce-copy writes into the
+next rank's FIFO. On the one-GPU test box all ranks share cuda:0, so the peer path is exercised
+through IPC mappings on one device; across GPUs the same mappings go over xGMI.
+
+Each rank runs in a child process (tests/peer_ring_worker.py); outputs are compared bit for bit with
+the ring fold-order oracle, for every rank and for a second, in-place call on the same communicator.
+"""
+import os
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "peer_ring_worker.py")
+
+
+def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7):
+    name = f"/nexr_test_{uuid.uuid4().hex[:16]}"
+    out = [str(tmp_path / f"rank{r}") for r in range(n)]
+    procs = []
+    try:
+        for r in range(n):
+            cmd = [sys.executable, WORKER, "--rank", str(r), "--n", str(n), "--dt", str(dt), "--op", str(op),
+                   "--count", str(count), "--seed", str(seed), "--proto", str(proto), "--buff", str(buff),
+                   "--calls", str(calls), "--shm", name, "--out", out[r]]
+            procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+        logs = []
+        for p in procs:
+            try:
+                logs.append(p.communicate(timeout=300)[0])
+            except subprocess.TimeoutExpired:
+                p.kill()
+                logs.append(p.communicate()[0])
+        for r, p in enumerate(procs):
+            assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        shm_path = "/dev/shm" + name
+        if os.path.exists(shm_path):
+            os.unlink(shm_path)
+    return [[np.load(f"{out[r]}.{c}.npy") for c in range(calls)] for r in range(n)]
+
+
+@pytest.mark.parametrize("n,dt,op,proto", [(2, mg.F32, 0, 0), (3, mg.BF16, 0, 0), (4, mg.I32, 3, 0),
+                                           (2, mg.F16, 4, 0), (3, mg.F32, 0, 1), (2, mg.BF16, 0, 2),
+                                           (4, mg.I8, 2, 1)])
+def test_peer_ring_processes_match_fold_order(oracle, tmp_path, n, dt, op, proto):
+    from oracle.ring import ring_allreduce_expected, ring_allreduce_expected_ll
+    count = 200_003
+    buff = {0: 1 << 18, 1: 8 * 16 * 512, 2: 8 * 2048 * 8}[proto]
+    outs = _run_ring(tmp_path, n, dt, op, count, proto, buff)
+
+    def expected(inputs):
+        if proto == 0:
+            return ring_allreduce_expected(inputs, dt, op, buff)
+        return ring_allreduce_expected_ll(inputs, dt, op, buff, proto="ll" if proto == 1 else "ll128")
+
+    inputs = mg.gen_inputs(dt, n, count, 7, special=True)
+    exp0 = expected(inputs)
+    exp1 = expected([exp0[r] for r in range(n)])
+    for r in range(n):
+        assert mg.canon_bytes(dt, outs[r][0]) == mg.canon_bytes(dt, exp0[r]), f"rank {r}, call 0"
+        assert mg.canon_bytes(dt, outs[r][1]) == mg.canon_bytes(dt, exp1[r]), f"rank {r}, call 1 (in place)"
+
+
+def test_peer_ring_c1_two_processes_fp32_sum(tmp_path):
+    # BASELINE configs[0] (fp32 sum all-reduce, 4 MiB, 2 ranks) with real process ranks.
+    count = 1 << 20
+    outs = _run_ring(tmp_path, 2, mg.F32, 0, count, 0, 0, calls=1, seed=4242)
+    inputs = mg.gen_inputs(mg.F32, 2, count, 4242, special=True)
+    with np.errstate(over="ignore", invalid="ignore"):  # special values include inf and NaN
+        exp = (inputs[0] + inputs[1]).astype(np.float32)
+    for r in range(2):
+        assert mg.canon_bytes(mg.F32, outs[r][0]) == mg.canon_bytes(mg.F32, exp), f"rank {r}"
