@@ -156,6 +156,40 @@ def test_torch_layer_and_streams(nexr, oracle, dev):
     assert same(mg.F32, o.cpu().numpy(), exp)
 
 
+def test_hip_graph_capture_and_replay(nexr, oracle, dev):
+    # nexrReduceCopy and nexrReduceCopyBatch are plain stream-ordered launches, so a HIP graph can
+    # capture a chain of them (here: a K=2 sum feeding a K=3 max, plus a batch of small works) and
+    # replay it on new data in place.
+    n = 300_001
+    a, b, c = (torch.randn(n, device="cuda") for _ in range(3))
+    t = torch.empty_like(a)
+    o = torch.empty_like(a)
+    small_in = [torch.randn(1000 + i, device="cuda") for i in range(6)]
+    small_out = [torch.empty_like(x) for x in small_in]
+    max_arg = mg.minmax_arg(mg.F32, True)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nexr.reduce_copy([a, b], [t], nexr.DevRedOp.Sum)
+        nexr.reduce_copy([t, c, a], [o], nexr.DevRedOp.MinMax, red_op_arg=max_arg)
+        works = [nexr.make_work([x.data_ptr(), x.data_ptr()], [y.data_ptr()], x.numel())
+                 for x, y in zip(small_in, small_out)]
+        nexr.reduce_copy_batch(works, nexr.DataType.Float32, nexr.DevRedOp.Sum,
+                               torch.cuda.current_stream().cuda_stream)
+    for rep in range(3):
+        for x in (a, b, c, *small_in):
+            x.copy_(torch.randn_like(x))
+        g.replay()
+        torch.cuda.synchronize()
+        an, bn, cn = (x.cpu().numpy() for x in (a, b, c))
+        tn = oracle.reduce_copy([an, bn], 1, mg.F32, mg.SUM)[0]
+        on = oracle.reduce_copy([tn, cn, an], 1, mg.F32, mg.MINMAX, max_arg)[0]
+        assert same(mg.F32, t.cpu().numpy(), tn) and same(mg.F32, o.cpu().numpy(), on), rep
+        for x, y in zip(small_in, small_out):
+            xn = x.cpu().numpy()
+            assert same(mg.F32, y.cpu().numpy(), oracle.reduce_copy([xn, xn], 1, mg.F32, mg.SUM)[0]), rep
+
+
 def test_concurrent_callers_on_separate_streams(nexr, oracle, dev):
     n = 1 << 18
     jobs = []

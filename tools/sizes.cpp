@@ -3,6 +3,7 @@
 //   hipcc -O2 -std=c++17 tools/sizes.cpp -Lnex-nccl_amd -lnexr -Wl,-rpath,$PWD/nex-nccl_amd -o tools/sizes
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -51,8 +52,8 @@ int main() {
 
   // Batched: W independent works of `bytes` each, one nexrReduceCopyBatch call vs W nexrReduceCopy calls.
   const int W = NEXR_MAX_BATCH_WORKS;
-  printf("\nbatch of %d works (fp32 sum K=2 M=1)\n%12s %14s %14s %14s %14s\n", W, "bytes/work", "sep us/work",
-         "batch us/work", "sep GB/s", "batch GB/s");
+  printf("\nbatch of %d works (fp32 sum K=2 M=1)\n%12s %14s %14s %14s %14s %14s %14s\n", W, "bytes/work",
+         "sep us/work", "batch us/work", "graph us/work", "host us/call", "sep GB/s", "batch GB/s");
   const size_t bsizes[] = {4 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20};
   for (size_t bytes : bsizes) {
     std::vector<void*> a(W), b(W), o(W);
@@ -72,14 +73,33 @@ int main() {
         nexrReduceCopy(2, works[w].srcs, 1, works[w].dsts, works[w].nElts, nexrFloat32, nexrDevSum, 0, 0, nullptr, 0, s);
     };
     auto bat = [&]() { nexrReduceCopyBatch(works.data(), W, nexrFloat32, nexrDevSum, s); };
-    float res[2];
-    for (int mode = 0; mode < 2; mode++) {
-      for (int i = 0; i < 10; i++) mode ? bat() : sep();
+    // mode 2: the W separate calls captured once into a HIP graph and replayed.
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    sep();
+    CK(hipStreamEndCapture(s, &graph));
+    CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    auto run = [&](int mode) {
+      if (mode == 0) sep();
+      else if (mode == 1) bat();
+      else (void)hipGraphLaunch(exec, s);
+    };
+    // host-side cost of one nexrReduceCopy call (enqueue only)
+    CK(hipStreamSynchronize(s));
+    auto h0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < 200; i++) sep();
+    auto h1 = std::chrono::steady_clock::now();
+    CK(hipStreamSynchronize(s));
+    const double hostUs = std::chrono::duration<double, std::micro>(h1 - h0).count() / (200.0 * W);
+    float res[3];
+    for (int mode = 0; mode < 3; mode++) {
+      for (int i = 0; i < 10; i++) run(mode);
       CK(hipStreamSynchronize(s));
       std::vector<float> best;
       for (int rep = 0; rep < 5; rep++) {
         CK(hipEventRecord(e0, s));
-        for (int i = 0; i < iters; i++) mode ? bat() : sep();
+        for (int i = 0; i < iters; i++) run(mode);
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -89,8 +109,10 @@ int main() {
       std::sort(best.begin(), best.end());
       res[mode] = best[best.size() / 2];
     }
-    printf("%12zu %14.3f %14.3f %14.1f %14.1f\n", bytes, res[0] * 1e3, res[1] * 1e3, 3.0 * bytes / res[0] / 1e6,
-           3.0 * bytes / res[1] / 1e6);
+    printf("%12zu %14.3f %14.3f %14.3f %14.3f %14.1f %14.1f\n", bytes, res[0] * 1e3, res[1] * 1e3, res[2] * 1e3, hostUs,
+           3.0 * bytes / res[0] / 1e6, 3.0 * bytes / res[1] / 1e6);
+    CK(hipGraphExecDestroy(exec));
+    CK(hipGraphDestroy(graph));
     for (int w = 0; w < W; w++) { (void)hipFree(a[w]); (void)hipFree(b[w]); (void)hipFree(o[w]); }
   }
   return 0;
