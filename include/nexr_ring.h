@@ -1,9 +1,14 @@
 /*
- * nexr_ring.h — CPU-emulated ring all-reduce that drives the reduce-copy ABI (include/nexr.h)
- * from the reference's own schedule: the caller side of the drop-in boundary.
+ * nexr_ring.h — CPU-emulated collectives that drive the reduce-copy ABI (include/nexr.h) from the
+ * reference's own schedules: the caller side of the drop-in boundary.
  *
- * It restates, on host threads (one per emulated rank, 1 channel, SIMPLE protocol):
- *   - runRing for ncclAllReduce (reference src/device/all_reduce.h:12-84),
+ * It restates, on host threads (one per emulated rank, two for a non-root tree rank, 1 channel):
+ *   - runRing for ncclAllReduce (reference src/device/all_reduce.h:12-84), ncclReduceScatter
+ *     (reduce_scatter.h:12-52), ncclAllGather (all_gather.h:12-66), ncclReduce (reduce.h:12-50) and
+ *     ncclBroadcast (broadcast.h:12-58),
+ *   - runTreeSplit for the tree ncclAllReduce (all_reduce.h:150-230) over the reference's tree
+ *     topology: an intra-node chain (graph/connect.cc:51-61) whose node heads are joined by the
+ *     double binary tree (graph/trees.cc:31-109, connect.cc:95-163),
  *   - Primitives::genericOp slicing and the reduceCopy call sites (src/device/prims_simple.h:190-330,
  *     directSend/directRecvReduceDirectSend/directRecvReduceCopyDirectSend/directRecvCopyDirectSend/
  *     directRecv :897-976),
@@ -64,6 +69,9 @@ typedef struct {
   int protocol;        /* nexrRingProto_t (0 = SIMPLE) */
   nexrReduceCopyLLFn llFn; /* LL: NULL = nexrReduceCopyLL (device memory mode only) */
   nexrReduceCopyLL128Fn ll128Fn; /* LL128: NULL = nexrReduceCopyLL128 (device memory mode only) */
+  int treeRanksPerNode; /* tree topology: ranks per emulated node (0 = all ranks on one node, i.e. a
+                           chain); must divide nRanks. Node heads form the double binary tree */
+  int treeIndex;        /* which tree of the double binary tree: 0 (the btree) or 1 (mirror/shift) */
 } nexrRingConfig;
 
 typedef struct nexrRingComm* nexrRingComm_t;
@@ -75,6 +83,34 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* comm, const nexrRingCon
  * (host or device memory per memMode; in-place allowed). op is an ncclRedOp_t built-in. */
 NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op);
+
+/* ncclReduceScatter: rank r's sendbuffs[r] holds nRanks*recvcount elements; recvbuffs[r] receives the
+ * reduction of every rank's segment r (recvcount elements). */
+NEXR_API nexrResult_t nexrRingReduceScatter(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                            size_t recvcount, int datatype, int op);
+
+/* ncclAllGather: recvbuffs[r] (nRanks*sendcount elements) receives every rank's sendbuff in rank order;
+ * in place when sendbuffs[r] == recvbuffs[r] + r*sendcount elements. */
+NEXR_API nexrResult_t nexrRingAllGather(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t sendcount, int datatype);
+
+/* ncclReduce: recvbuffs[root] receives the reduction; other ranks' recvbuffs are not touched (may be NULL). */
+NEXR_API nexrResult_t nexrRingReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                     size_t count, int datatype, int op, int root);
+
+/* ncclBroadcast: every recvbuffs[r] receives sendbuffs[root] (other ranks' sendbuffs may be NULL). */
+NEXR_API nexrResult_t nexrRingBroadcast(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t count, int datatype, int root);
+
+/* ncclAllReduce with NCCL_ALGO_TREE: runTreeSplit over the topology of config->treeRanksPerNode /
+ * treeIndex. The reduce-up and broadcast-down halves of a non-root rank run on two threads, as the
+ * reference splits a block's threads between them. */
+NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t count, int datatype, int op);
+
+/* The tree links of `rank` in this communicator's topology: *up (-1 at the root) and down[0..2]
+ * (-1 when absent, children packed first as setTreeDown does). */
+NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t comm, int rank, int* up, int* down);
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t comm);
 
@@ -106,6 +142,16 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* comm, const nexrPee
 /* ncclAllReduce for this process's rank (sendbuff/recvbuff on config->device; in-place allowed). */
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int op);
+
+/* The other ring collectives for this process's rank, arguments as in the thread-rank versions. */
+NEXR_API nexrResult_t nexrPeerRingReduceScatter(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
+                                                size_t recvcount, int datatype, int op);
+NEXR_API nexrResult_t nexrPeerRingAllGather(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
+                                            size_t sendcount, int datatype);
+NEXR_API nexrResult_t nexrPeerRingReduce(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
+                                         int datatype, int op, int root);
+NEXR_API nexrResult_t nexrPeerRingBroadcast(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
+                                            int datatype, int root);
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,8 @@
-// nexr_ring.cpp — CPU-emulated ring all-reduce (include/nexr_ring.h): the reference's own
-// collective schedule, restated on host threads, calling the reduce-copy ABI at exactly the
-// reduceCopy sites of Primitives::genericOp. This is the drop-in demonstration for BASELINE
-// configs[0] ("fp32 sum all-reduce, 4 MiB, 2 CPU-emulated ranks"): the schedule is unchanged,
-// only the primitive underneath is the MI355X kernel.
+// nexr_ring.cpp — CPU-emulated collectives (include/nexr_ring.h): the reference's own collective
+// schedules, restated on host threads, calling the reduce-copy ABI at exactly the reduceCopy sites
+// of Primitives::genericOp. This is the drop-in demonstration for BASELINE configs[0] ("fp32 sum
+// all-reduce, 4 MiB, 2 CPU-emulated ranks") and for every other caller of the primitive: the
+// schedules are unchanged, only the primitive underneath is the MI355X kernel.
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <stdlib.h>
@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -22,23 +23,36 @@
 namespace {
 
 constexpr int kSteps = 8;                                // NCCL_STEPS (src/include/device.h:649)
-constexpr int kSliceSteps = kSteps / 4;                  // ALLREDUCE_SLICESTEPS (collectives.h:17)
-constexpr int kChunkSteps = kSteps / 2;                  // ALLREDUCE_CHUNKSTEPS (collectives.h:18)
-constexpr int kSlicePerChunk = kChunkSteps / kSliceSteps;
+constexpr int kMaxArity = 3;                             // NCCL_MAX_TREE_ARITY (device.h:185)
 constexpr size_t kDefaultBuffBytes = 4u << 20;           // NCCL_BUFFSIZE default (init.cc:620-634)
 constexpr size_t kDefaultLLBuffBytes = 8 * 512 * kSteps * 16;  // DEFAULT_LL_BUFFSIZE (init.cc:618)
 constexpr size_t kDefaultLL128BuffBytes = 120 * 640 * kSteps * 8;  // DEFAULT_LL128_BUFFSIZE (init.cc:619)
+constexpr size_t kMinBuffBytes = kSteps * 512;           // one SIMPLE grain per step at least
 
-// One directed connection prev -> r. The FIFO belongs to the receiver (the sender writes into it,
-// like a P2P/SHM transport's recv buffer, src/include/device.h:753-771).
+// ProtoSimple<SlicePerChunk = chunkSteps/sliceSteps, StepPerSlice = sliceSteps> of a collective
+// (src/include/collectives.h:16-25); LL and LL128 move one step per primitive call.
+struct Geom {
+  int chunkSteps, sliceSteps;
+};
+constexpr Geom kGeomRing{kSteps / 2, kSteps / 4};  // ALLREDUCE/ALLGATHER/REDUCESCATTER_*STEPS
+constexpr Geom kGeomPipe{1, 1};                    // BROADCAST/REDUCE_*STEPS; the tree's ProtoSimple<1,1>
+
+// One directed connection. The FIFO belongs to the receiver (the sender writes into it, like a
+// P2P/SHM transport's recv buffer, src/include/device.h:753-771).
 struct ConnState {
   alignas(64) std::atomic<uint64_t> tail{0};  // steps published by the sender   (postPeer, Send)
   alignas(64) std::atomic<uint64_t> head{0};  // steps released by the receiver  (postPeer, Recv)
 };
 struct Conn {
   char* fifo = nullptr;
+  int device = 0;        // device of the FIFO (device memory mode)
+  bool ownsFifo = true;  // false for a peer process's FIFO mapped over IPC
   ConnState own;
   ConnState* st = &own;  // the counters: `own` for thread ranks, a shared-memory slot for process ranks
+  // Each endpoint's step (the conn->step a Primitives loads and saves, prims_simple.h:528-560): only
+  // the sending thread touches sendStep and only the receiving thread touches recvStep.
+  alignas(64) uint64_t sendStep = 0;
+  alignas(64) uint64_t recvStep = 0;
 };
 
 // Process ranks (nexrPeerRingCommCreate): one POSIX shared-memory segment per communicator holds
@@ -64,19 +78,101 @@ PeerSlot* peerSlot(void* base, int r) { return (PeerSlot*)((char*)base + sizeof(
 int64_t divUp(int64_t a, int64_t b) { return (a + b - 1) / b; }
 int64_t alignUp(int64_t a, int64_t b) { return divUp(a, b) * b; }
 
+struct TreeLinks {
+  int up = -1;
+  int down[kMaxArity] = {-1, -1, -1};
+  int nDown() const {
+    int k = 0;
+    while (k < kMaxArity && down[k] >= 0) k++;
+    return k;
+  }
+};
+
+// ncclGetBtree (src/graph/trees.cc:31-63): the binary tree over nranks with root 0.
+void getBtree(int nranks, int rank, int* u, int* d0, int* d1) {
+  int bit;
+  for (bit = 1; bit < nranks; bit <<= 1)
+    if (bit & rank) break;
+  if (rank == 0) {
+    *u = -1;
+    *d0 = -1;
+    *d1 = nranks > 1 ? bit >> 1 : -1;
+    return;
+  }
+  int up = (rank ^ bit) | (bit << 1);
+  if (up >= nranks) up = (rank ^ bit);
+  *u = up;
+  int lowbit = bit >> 1;
+  *d0 = lowbit == 0 ? -1 : rank - lowbit;
+  int down1 = lowbit == 0 ? -1 : rank + lowbit;
+  while (down1 >= nranks) {
+    down1 = lowbit == 0 ? -1 : rank + lowbit;
+    lowbit >>= 1;
+  }
+  *d1 = down1;
+}
+
+// ncclGetDtree (trees.cc:86-109): tree 0 is the btree, tree 1 its mirror (even nranks) or shift (odd).
+void getDtree(int nranks, int rank, int t, int* u, int* d0, int* d1) {
+  if (t == 0) {
+    getBtree(nranks, rank, u, d0, d1);
+  } else if (nranks % 2 == 1) {
+    int uu, a, b;
+    getBtree(nranks, (rank - 1 + nranks) % nranks, &uu, &a, &b);
+    *u = uu == -1 ? -1 : (uu + 1) % nranks;
+    *d0 = a == -1 ? -1 : (a + 1) % nranks;
+    *d1 = b == -1 ? -1 : (b + 1) % nranks;
+  } else {
+    int uu, a, b;
+    getBtree(nranks, nranks - 1 - rank, &uu, &a, &b);
+    *u = uu == -1 ? -1 : nranks - 1 - uu;
+    *d0 = a == -1 ? -1 : nranks - 1 - a;
+    *d1 = b == -1 ? -1 : nranks - 1 - b;
+  }
+}
+
+// The tree of every rank: within a node of L ranks a chain (connect.cc:51-61: up = previous,
+// down[0] = next), and between nodes the double binary tree joining the node heads
+// (connectTrees, connect.cc:140-163, with the NCCL_TOPO_PATTERN_TREE head as parent and both
+// children) whose children are packed after the chain child by setTreeDown (:111-121).
+std::vector<TreeLinks> treeTopology(int nRanks, int L, int t) {
+  std::vector<TreeLinks> links(nRanks);
+  const int nNodes = nRanks / L;
+  for (int r = 0; r < nRanks; r++) {
+    TreeLinks& k = links[r];
+    const int node = r / L, i = r % L;
+    k.up = i == 0 ? -1 : r - 1;
+    k.down[0] = i == L - 1 ? -1 : r + 1;
+    if (i == 0) {
+      int u, d0, d1;
+      getDtree(nNodes, node, t, &u, &d0, &d1);
+      if (u != -1) k.up = u * L;
+      for (int d : {d0, d1}) {
+        if (d == -1) continue;
+        int x = 0;
+        while (x < kMaxArity && k.down[x] >= 0) x++;
+        if (x < kMaxArity) k.down[x] = d * L;
+      }
+    }
+  }
+  return links;
+}
+
 }  // namespace
 
 struct nexrRingComm {
   nexrRingConfig cfg;
   size_t stepBytes = 0;
-  std::vector<Conn*> conns;          // conns[r]: connection into rank r from rank r-1
-  std::vector<uint64_t> recvStep;    // per rank: next step to consume from conns[r]
-  std::vector<uint64_t> sendStep;    // per rank: next step to produce into conns[(r+1)%n]
+  std::vector<Conn*> conns;     // ring: conns[r] is the connection into rank r from rank r-1
+  std::vector<TreeLinks> tree;  // tree topology (computed at creation)
+  std::vector<Conn*> treeUp;    // treeUp[r]: r -> parent(r) (reduce); created by the first tree call
+  std::vector<Conn*> treeDown;  // treeDown[r]: parent(r) -> r (broadcast)
   std::vector<int> devices;
-  std::vector<hipStream_t> streams;
-  std::vector<uint32_t*> status;     // LL: per-rank pinned status word the kernel reports timeouts in
+  std::vector<hipStream_t> streams, streams2;  // streams2: the tree's broadcast-half threads
+  std::vector<uint32_t*> status, status2;      // LL: pinned status words the kernel reports timeouts in
   bool ll = false;     // LL or LL128: one FIFO step per primitive call, data readiness in line flags
   int proto = nexrRingProtoSimple;
+  bool needHip = false;
   bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
   bool broken = false;
   // Process ranks: this process is rank `self` only.
@@ -85,8 +181,6 @@ struct nexrRingComm {
   void* shm = nullptr;
   size_t shmBytes = 0;
   char shmName[256] = {0};
-  char* peerFifo = nullptr;  // the next rank's FIFO, IPC-mapped into this process
-  bool peerFifoIpc = false;
 };
 
 namespace {
@@ -106,17 +200,23 @@ struct Shared {
   }
 };
 
-// One rank's Primitives<T, RedOp, FanSymmetric<1>, 1, ProtoSimple> (prims_simple.h), host side.
+enum { kNone = -1, kInput = 0, kOutput = 1 };  // SrcBuf / DstBuf of genericOp
+
+// One rank's Primitives<T, RedOp, Fan, Direct, Proto> (prims_simple.h / prims_ll.h / prims_ll128.h),
+// host side: up to kMaxArity recv peers and kMaxArity send peers (FanAsymmetric of the tree).
 struct Prims {
   nexrRingComm* c;
   Shared* sh;
   int rank;
-  Conn* recvConn;
-  Conn* sendConn;
+  Conn* recv[kMaxArity];
+  int nRecv = 0;
+  Conn* send[kMaxArity];
+  int nSend = 0;
   const char* userInput;
   char* userOutput;
   size_t esz;
   int64_t stepSize;  // elements per FIFO step (prims_simple.h:607)
+  int stepPerSlice = 1, slicePerChunk = 1;
   int datatype, devOp;
   uint64_t redOpArgs[1];
   nexrReduceCopyFn fn;
@@ -125,6 +225,8 @@ struct Prims {
   uint32_t* status;
   hipStream_t stream;
   bool device;
+
+  char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
 
   // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
   // abortable like checkAbort (primitives.h:142-156).
@@ -148,42 +250,39 @@ struct Prims {
   }
 
   // genericOp<DirectRecv=0, DirectSend=0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330),
-  // with the non-direct FIFO pointers (waitPeer :150-164 default branch).
-  bool genericOp(bool Recv, bool Send, bool Src, bool Dst, int64_t srcIx, int64_t dstIx, int64_t nelem,
+  // with the non-direct FIFO pointers (waitPeer :150-164 default branch). srcs = [user src, recv
+  // peers...], dsts = [user dst, send peers...] (:131-132, :238-242).
+  bool genericOp(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t nelem,
                  bool postOp) {
+    const int nr = Recv ? nRecv : 0, ns = Send ? nSend : 0;
     nelem = nelem < 0 ? 0 : nelem;
-    int64_t sliceSize = stepSize * kSliceSteps;
-    sliceSize = std::max(divUp(nelem, 16 * kSlicePerChunk) * 16, sliceSize / 32);
+    int64_t sliceSize = stepSize * stepPerSlice;
+    sliceSize = std::max(divUp(nelem, 16 * slicePerChunk) * 16, sliceSize / 32);
     int64_t offset = 0;
-    for (int slice = 0; slice < kSlicePerChunk; slice++) {
+    for (int slice = 0; slice < slicePerChunk; slice++) {
       sliceSize = std::min(sliceSize, nelem - offset);
       if (sliceSize < 0) sliceSize = 0;
-      uint64_t& rs = c->recvStep[rank];
-      uint64_t& ss = c->sendStep[rank];
-      const char* recvPtr = nullptr;
-      char* sendPtr = nullptr;
-      if (Recv) {  // wait for the peer's data: tail >= step + StepPerSlice
-        if (!waitAtLeast(recvConn->st->tail, rs + kSliceSteps)) return false;
-        recvPtr = recvConn->fifo + (rs % kSteps) * c->stepBytes;
+      const void* srcs[1 + kMaxArity];
+      void* dsts[1 + kMaxArity];
+      int k = 0, m = 0;
+      if (srcBuf != kNone) srcs[k++] = buf(srcBuf) + (srcIx + offset) * esz;
+      if (dstBuf != kNone) dsts[m++] = buf(dstBuf) + (dstIx + offset) * esz;
+      for (int i = 0; i < nr; i++) {  // wait for the peer's data: tail >= step + StepPerSlice
+        Conn* q = recv[i];
+        if (!waitAtLeast(q->st->tail, q->recvStep + stepPerSlice)) return false;
+        srcs[k++] = q->fifo + (q->recvStep % kSteps) * c->stepBytes;
       }
-      if (Send) {  // wait for credit: head + NCCL_STEPS >= step + StepPerSlice
-        if (ss + kSliceSteps > (uint64_t)kSteps && !waitAtLeast(sendConn->st->head, ss + kSliceSteps - kSteps))
+      for (int i = 0; i < ns; i++) {  // wait for credit: head + NCCL_STEPS >= step + StepPerSlice
+        Conn* q = send[i];
+        if (q->sendStep + stepPerSlice > (uint64_t)kSteps &&
+            !waitAtLeast(q->st->head, q->sendStep + stepPerSlice - kSteps))
           return false;
-        sendPtr = sendConn->fifo + (ss % kSteps) * c->stepBytes;
+        dsts[m++] = q->fifo + (q->sendStep % kSteps) * c->stepBytes;
       }
-      if (sliceSize > 0) {
-        // srcs: local buffer at index 0 (if Src), peers after it; dsts: user output at 0 (if Dst),
-        // next peer after it (prims_simple.h:131-132, :238-242).
-        const void* srcs[2];
-        void* dsts[2];
-        int ns = 0, nd = 0;
-        if (Src) srcs[ns++] = userInput + (srcIx + offset) * esz;
-        if (Recv) srcs[ns++] = recvPtr;
-        if (Dst) dsts[nd++] = userOutput + (dstIx + offset) * esz;
-        if (Send) dsts[nd++] = sendPtr;
+      if (sliceSize > 0 && k > 0 && m > 0) {
         // PreOpSrcs = SrcBuf != Input ? 0 : 1 (prims_simple.h:279-280); preOpArgs = redOpArgs.
-        const int nPre = Src ? 1 : 0;
-        nexrResult_t r = fn(ns, srcs, nd, dsts, (size_t)sliceSize, datatype, devOp, redOpArgs[0], nPre,
+        const int nPre = srcBuf == kInput ? 1 : 0;
+        nexrResult_t r = fn(k, srcs, m, dsts, (size_t)sliceSize, datatype, devOp, redOpArgs[0], nPre,
                             nPre ? redOpArgs : nullptr, postOp ? 1 : 0, (nexrStream_t)stream);
         if (r == nexrSuccess && device) {
           hipError_t e = hipStreamSynchronize(stream);  // data complete before the step is posted
@@ -195,48 +294,61 @@ struct Prims {
         }
       }
       // postPeer (prims_simple.h:177-188): release the slot / publish the data.
-      if (Recv) {
-        rs += kSliceSteps;
-        recvConn->st->head.store(rs, std::memory_order_release);
+      for (int i = 0; i < nr; i++) {
+        recv[i]->recvStep += stepPerSlice;
+        recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
       }
-      if (Send) {
-        ss += kSliceSteps;
-        sendConn->st->tail.store(ss, std::memory_order_release);
+      for (int i = 0; i < ns; i++) {
+        send[i]->sendStep += stepPerSlice;
+        send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
       }
       offset += sliceSize;
     }
     return true;
   }
-  // LLGenericOp<RECV, SEND, SrcBuf, DstBuf> (prims_ll.h:218-283): one FIFO step per call. The
-  // sender waits for a credit (waitSend :55-75); the receiver's data readiness is the line flags
-  // NCCL_LL_FLAG(step+1) (:42-43). The host additionally waits for the sender's step so that the
-  // kernel's flag poll succeeds at once: two emulated ranks may share one GPU, and a kernel spinning
-  // on a producer that cannot be scheduled beside it must never be launched.
-  bool genericOpLL(bool Recv, bool Send, bool Src, bool Dst, int64_t srcIx, int64_t dstIx, int64_t nelem,
+  // LLGenericOp<RECV, SEND, SrcBuf, DstBuf> (prims_ll.h:218-283) / GenericOp of prims_ll128.h
+  // (:294-331): one FIFO step per call. The sender waits for a credit (waitSend :55-75); the
+  // receiver's data readiness is the line flags (NCCL_LL_FLAG(step+1), :42-43; step+1 for LL128).
+  // The host additionally waits for the sender's step so that the kernel's flag poll succeeds at
+  // once: two emulated ranks may share one GPU, and a kernel spinning on a producer that cannot be
+  // scheduled beside it must never be launched.
+  bool genericOpLL(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t nelem,
                    bool postOp) {
+    const int nr = Recv ? nRecv : 0, ns = Send ? nSend : 0;
     nelem = nelem < 0 ? 0 : nelem;
-    uint64_t& rs = c->recvStep[rank];
-    uint64_t& ss = c->sendStep[rank];
-    if (Send && ss + 1 > (uint64_t)kSteps && !waitAtLeast(sendConn->st->head, ss + 1 - kSteps)) return false;
-    if (Recv && !waitAtLeast(recvConn->st->tail, rs + 1)) return false;
+    for (int i = 0; i < ns; i++) {
+      Conn* q = send[i];
+      if (q->sendStep + 1 > (uint64_t)kSteps && !waitAtLeast(q->st->head, q->sendStep + 1 - kSteps)) return false;
+    }
+    for (int i = 0; i < nr; i++)
+      if (!waitAtLeast(recv[i]->st->tail, recv[i]->recvStep + 1)) return false;
     if (nelem > 0) {
-      const void* recvLines[1] = {recvConn->fifo + (rs % kSteps) * c->stepBytes};
-      void* sendLines[1] = {sendConn->fifo + (ss % kSteps) * c->stepBytes};
-      const uint32_t recvFlag[1] = {(uint32_t)(rs + 1)};  // NCCL_LL_FLAG(recvStep+1)
-      const uint32_t sendFlag[1] = {(uint32_t)(ss + 1)};
+      const void* recvLines[kMaxArity];
+      void* sendLines[kMaxArity];
+      uint32_t rf32[kMaxArity], sf32[kMaxArity];
+      uint64_t rf64[kMaxArity], sf64[kMaxArity];
+      for (int i = 0; i < nr; i++) {
+        recvLines[i] = recv[i]->fifo + (recv[i]->recvStep % kSteps) * c->stepBytes;
+        rf64[i] = recv[i]->recvStep + 1;
+        rf32[i] = (uint32_t)rf64[i];
+      }
+      for (int i = 0; i < ns; i++) {
+        sendLines[i] = send[i]->fifo + (send[i]->sendStep % kSteps) * c->stepBytes;
+        sf64[i] = send[i]->sendStep + 1;
+        sf32[i] = (uint32_t)sf64[i];
+      }
+      const void* src = srcBuf != kNone ? buf(srcBuf) + srcIx * esz : nullptr;
+      void* dst = dstBuf != kNone ? buf(dstBuf) + dstIx * esz : nullptr;
+      const int srcIsInput = srcBuf == kInput ? 1 : 0;
       if (status) *status = 0;
       const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
       nexrResult_t r;
-      if (c->proto == nexrRingProtoLL128) {  // 64-bit flags = step + 1 (prims_ll128.h:49-50)
-        const uint64_t rf[1] = {rs + 1}, sf[1] = {ss + 1};
-        r = ll128Fn(Src ? userInput + srcIx * esz : nullptr, Src ? 1 : 0, Recv ? 1 : 0, recvLines, rf,
-                    Dst ? userOutput + dstIx * esz : nullptr, Send ? 1 : 0, sendLines, sf, (size_t)nelem, datatype,
-                    devOp, redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
-      } else {
-        r = llFn(Src ? userInput + srcIx * esz : nullptr, Src ? 1 : 0, Recv ? 1 : 0, recvLines, recvFlag,
-                 Dst ? userOutput + dstIx * esz : nullptr, Send ? 1 : 0, sendLines, sendFlag, (size_t)nelem,
-                 datatype, devOp, redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
-      }
+      if (c->proto == nexrRingProtoLL128)
+        r = ll128Fn(src, srcIsInput, nr, recvLines, rf64, dst, ns, sendLines, sf64, (size_t)nelem, datatype, devOp,
+                    redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
+      else
+        r = llFn(src, srcIsInput, nr, recvLines, rf32, dst, ns, sendLines, sf32, (size_t)nelem, datatype, devOp,
+                 redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
       if (r == nexrSuccess && device && hipStreamSynchronize(stream) != hipSuccess) r = nexrUnhandledCudaError;
       if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
       if (r != nexrSuccess) {
@@ -244,39 +356,63 @@ struct Prims {
         return false;
       }
     }
-    if (Recv) {  // postRecv (:80-83)
-      rs += 1;
-      recvConn->st->head.store(rs, std::memory_order_release);
+    for (int i = 0; i < nr; i++) {  // postRecv (:80-83)
+      recv[i]->recvStep += 1;
+      recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
     }
-    if (Send) {  // incSend (:85-93); the flag-wrap cleanup at NCCL_LL_CLEAN_MASK needs ~2^31 steps
-      ss += 1;
-      sendConn->st->tail.store(ss, std::memory_order_release);
+    for (int i = 0; i < ns; i++) {  // incSend (:85-93); the flag-wrap cleanup at NCCL_LL_CLEAN_MASK needs ~2^31 steps
+      send[i]->sendStep += 1;
+      send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
     }
     return true;
   }
-  bool op(bool Recv, bool Send, bool Src, bool Dst, int64_t srcIx, int64_t dstIx, int64_t n, bool postOp) {
-    return c->ll ? genericOpLL(Recv, Send, Src, Dst, srcIx, dstIx, n, postOp)
-                 : genericOp(Recv, Send, Src, Dst, srcIx, dstIx, n, postOp);
+  bool op(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t n, bool postOp) {
+    return c->ll ? genericOpLL(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp)
+                 : genericOp(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp);
   }
-  bool directSend(int64_t inpIx, int64_t n) { return op(false, true, true, false, inpIx, -1, n, false); }
-  bool directRecvReduceDirectSend(int64_t inpIx, int64_t n) { return op(true, true, true, false, inpIx, -1, n, false); }
-  bool directRecvReduceCopyDirectSend(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
-    return op(true, true, true, true, inpIx, outIx, n, postOp);
+  // The primitives the schedules use (prims_simple.h:897-976; the direct* forms reduce to these
+  // without registered peer buffers).
+  bool sendInput(int64_t inpIx, int64_t n) { return op(false, true, kInput, kNone, inpIx, -1, n, false); }
+  bool copySend(int64_t inpIx, int64_t outIx, int64_t n) { return op(false, true, kInput, kOutput, inpIx, outIx, n, false); }
+  bool sendFromOutput(int64_t outIx, int64_t n) { return op(false, true, kOutput, kNone, outIx, -1, n, false); }
+  bool recvReduceSend(int64_t inpIx, int64_t n) { return op(true, true, kInput, kNone, inpIx, -1, n, false); }
+  bool recvReduceCopy(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
+    return op(true, false, kInput, kOutput, inpIx, outIx, n, postOp);
   }
-  bool directRecvCopyDirectSend(int64_t outIx, int64_t n) { return op(true, true, false, true, -1, outIx, n, false); }
-  bool directRecv(int64_t outIx, int64_t n) { return op(true, false, false, true, -1, outIx, n, false); }
+  bool recvReduceCopySend(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
+    return op(true, true, kInput, kOutput, inpIx, outIx, n, postOp);
+  }
+  bool recvCopySend(int64_t outIx, int64_t n) { return op(true, true, kNone, kOutput, -1, outIx, n, false); }
+  bool recvOutput(int64_t outIx, int64_t n) { return op(true, false, kNone, kOutput, -1, outIx, n, false); }
 };
 
-// runRing<T, RedOp, ProtoSimple> (all_reduce.h:12-84) for one rank, 1 channel (gridOffset 0,
-// channelCount = count, chunkCount = chunkSize / sizeof(T): enqueue.cc:1993-1996, :655-678).
-void runRing(Prims& p, int nranks, int64_t count) {
+// calcCollChunking for one channel (src/enqueue.cc:1993-1999; tree LL128 :2043-2051; grain
+// alignment :2062) → chunkCount in elements (ncclCollCbdPart, device.h:946-970).
+int64_t chunkElems(const nexrRingComm* c, Geom g, size_t esz, bool tree, size_t nBytes) {
+  int64_t chunk = (int64_t)c->stepBytes * (c->proto == nexrRingProtoSimple ? g.chunkSteps : 1);
+  if (c->proto == nexrRingProtoLL) chunk /= 2;
+  if (c->proto == nexrRingProtoLL128) chunk = chunk / 16 * 15;  // NCCL_LL128_LINEELEMS / DATAELEMS
+  if (tree && c->proto == nexrRingProtoLL128) {
+    const int L = c->cfg.treeRanksPerNode > 0 ? c->cfg.treeRanksPerNode : c->cfg.nRanks;
+    const int nNodes = c->cfg.nRanks / L;
+    int log2n = 0;
+    while ((2 << log2n) <= nNodes) log2n++;
+    const float ppn = (float)c->cfg.nRanks / (float)nNodes;
+    const float nstepsLL128 = 1 + log2n + 0.1f * ppn;
+    while ((float)(nBytes / (size_t)chunk) < nstepsLL128 * 64 / ppn && chunk > 131072) chunk /= 2;
+    while ((float)(nBytes / (size_t)chunk) < nstepsLL128 * 16 / ppn && chunk > 32768) chunk /= 2;
+  }
+  const int64_t grain = c->proto == nexrRingProtoLL ? 16 : c->proto == nexrRingProtoLL128 ? 1920 : 512;
+  chunk = chunk / grain * grain;
+  return chunk / (int64_t)esz;
+}
+
+// ---- schedules (one rank's view; 1 channel, userRanks[i] = (rank + i) % nranks) ----------------
+
+// runRing for ncclAllReduce (all_reduce.h:12-84).
+void runRingAllReduce(Prims& p, int nranks, int64_t count) {
   const int ringIx = p.rank;
-  // SIMPLE: chunkSize = stepSize * chunkSteps; LL: stepSize / 2; LL128: stepSize / 16 * 15, aligned
-  // to the 1920-B grain (enqueue.cc:1993-1999, :2062)
-  int64_t chunkBytes = (int64_t)(p.c->stepBytes * kChunkSteps);
-  if (p.c->proto == nexrRingProtoLL) chunkBytes = (int64_t)(p.c->stepBytes / 2);
-  if (p.c->proto == nexrRingProtoLL128) chunkBytes = (int64_t)(p.c->stepBytes / 16 * 15) / 1920 * 1920;
-  int64_t chunkCount = chunkBytes / (int64_t)p.esz;
+  int64_t chunkCount = chunkElems(p.c, kGeomRing, p.esz, false, 0);
   const int64_t loopCount = nranks * chunkCount;
   auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
   for (int64_t elemOffset = 0; elemOffset < count; elemOffset += loopCount) {
@@ -290,23 +426,108 @@ void runRing(Prims& p, int nranks, int64_t count) {
     int64_t offset, nelem;
     // step 0: push data to next GPU
     nelem = at(modRanks(ringIx + nranks - 1), &offset);
-    if (!p.directSend(offset, nelem)) return;
+    if (!p.sendInput(offset, nelem)) return;
     // k-2 steps: reduce and copy to next GPU
     for (int j = 2; j < nranks; ++j) {
       nelem = at(modRanks(ringIx + nranks - j), &offset);
-      if (!p.directRecvReduceDirectSend(offset, nelem)) return;
+      if (!p.recvReduceSend(offset, nelem)) return;
     }
     // step k-1: reduce this buffer and data -> final result, stored and pushed
     nelem = at(ringIx, &offset);
-    if (!p.directRecvReduceCopyDirectSend(offset, offset, nelem, /*postOp=*/true)) return;
+    if (!p.recvReduceCopySend(offset, offset, nelem, /*postOp=*/true)) return;
     // k-2 steps: copy to next GPU
     for (int j = 1; j < nranks - 1; ++j) {
       nelem = at(modRanks(ringIx + nranks - j), &offset);
-      if (!p.directRecvCopyDirectSend(offset, nelem)) return;
+      if (!p.recvCopySend(offset, nelem)) return;
     }
     // final copy from buffer to dest
     nelem = at(modRanks(ringIx + 1), &offset);
-    if (!p.directRecv(offset, nelem)) return;
+    if (!p.recvOutput(offset, nelem)) return;
+  }
+}
+
+// runRing for ncclReduceScatter (reduce_scatter.h:12-52): `count` is the per-rank recvcount; the
+// segment of rankDest starts at rankDest*count in every sendbuff.
+void runRingReduceScatter(Prims& p, int nranks, int64_t count) {
+  const int64_t chunkCount = chunkElems(p.c, kGeomRing, p.esz, false, 0);
+  const int r = p.rank;
+  for (int64_t elemOffset = 0; elemOffset < count; elemOffset += chunkCount) {
+    const int64_t nelem = std::min(chunkCount, count - elemOffset);
+    const int64_t dataOffset = elemOffset;
+    int rankDest = (r + nranks - 1) % nranks;  // ringRanks[nranks-1]
+    if (!p.sendInput(dataOffset + rankDest * count, nelem)) return;
+    for (int j = 2; j < nranks; ++j) {
+      rankDest = (r + nranks - j) % nranks;
+      if (!p.recvReduceSend(dataOffset + rankDest * count, nelem)) return;
+    }
+    rankDest = r;  // ringRanks[0]
+    if (!p.recvReduceCopy(dataOffset + rankDest * count, dataOffset, nelem, /*postOp=*/true)) return;
+  }
+}
+
+// runRing for ncclAllGather (all_gather.h:12-66): `count` is the per-rank sendcount.
+void runRingAllGather(Prims& p, int nranks, int64_t count) {
+  const int64_t chunkCount = chunkElems(p.c, kGeomRing, p.esz, false, 0);
+  const int r = p.rank;
+  for (int64_t elemOffset = 0; elemOffset < count; elemOffset += chunkCount) {
+    const int64_t nelem = std::min(chunkCount, count - elemOffset);
+    const int64_t dataOffset = elemOffset;
+    int64_t offset = dataOffset + (int64_t)r * count;
+    // in place when the input chunk already sits at its place in the output (:52-56)
+    const bool inPlace = p.userInput + dataOffset * p.esz == p.userOutput + offset * p.esz;
+    if (!(inPlace ? p.sendInput(dataOffset, nelem) : p.copySend(dataOffset, offset, nelem))) return;
+    for (int j = 1; j < nranks - 1; ++j) {
+      const int rankDest = (r + nranks - j) % nranks;
+      offset = dataOffset + (int64_t)rankDest * count;
+      if (!p.recvCopySend(offset, nelem)) return;
+    }
+    offset = dataOffset + (int64_t)((r + 1) % nranks) * count;
+    if (!p.recvOutput(offset, nelem)) return;
+  }
+}
+
+// runRing for ncclReduce (reduce.h:12-50).
+void runRingReduce(Prims& p, int nranks, int64_t count, int root) {
+  const int64_t chunkCount = chunkElems(p.c, kGeomPipe, p.esz, false, 0);
+  const int r = p.rank, prevRank = (r + nranks - 1) % nranks;
+  for (int64_t offset = 0; offset < count; offset += chunkCount) {
+    const int64_t nelem = std::min(chunkCount, count - offset);
+    bool ok;
+    if (prevRank == root) ok = p.sendInput(offset, nelem);
+    else if (r == root) ok = p.recvReduceCopy(offset, offset, nelem, /*postOp=*/true);
+    else ok = p.recvReduceSend(offset, nelem);
+    if (!ok) return;
+  }
+}
+
+// runRing for ncclBroadcast (broadcast.h:12-58).
+void runRingBroadcast(Prims& p, int nranks, int64_t count, int root) {
+  const int64_t chunkCount = chunkElems(p.c, kGeomPipe, p.esz, false, 0);
+  const int r = p.rank, nextRank = (r + 1) % nranks;
+  for (int64_t offset = 0; offset < count; offset += chunkCount) {
+    const int64_t nelem = std::min(chunkCount, count - offset);
+    bool ok;
+    if (r == root) ok = p.userInput == p.userOutput ? p.sendInput(offset, nelem) : p.copySend(offset, offset, nelem);
+    else if (nextRank == root) ok = p.recvOutput(offset, nelem);
+    else ok = p.recvCopySend(offset, nelem);
+    if (!ok) return;
+  }
+}
+
+// runTreeSplit for ncclAllReduce (all_reduce.h:150-230), one role of one rank: the root reduces
+// from and broadcasts to its children in one pass (FanSymmetric<NCCL_MAX_TREE_ARITY_TOP>); every
+// other rank runs a reduce-up half (FanAsymmetric<3,1>) and a broadcast-down half
+// (FanAsymmetric<1,3>) side by side.
+enum TreeRole { kTreeRoot, kTreeReduceUp, kTreeBcastDown };
+void runTree(Prims& p, int64_t count, TreeRole role, bool leaf) {
+  const int64_t chunkCount = chunkElems(p.c, kGeomPipe, p.esz, true, (size_t)count * p.esz);
+  for (int64_t offset = 0; offset < count; offset += chunkCount) {
+    const int64_t nelem = std::min(chunkCount, count - offset);
+    bool ok;
+    if (role == kTreeRoot) ok = p.recvReduceCopySend(offset, offset, nelem, /*postOp=*/true);
+    else if (role == kTreeReduceUp) ok = leaf ? p.sendInput(offset, nelem) : p.recvReduceSend(offset, nelem);
+    else ok = leaf ? p.recvOutput(offset, nelem) : p.recvCopySend(offset, nelem);
+    if (!ok) return;
   }
 }
 
@@ -333,31 +554,32 @@ nexrResult_t defaultDeviceFn(int nSrcs, const void* const* srcs, int nDsts, void
   return nexrReduceCopy(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
 }
 
-Prims makePrims(nexrRingComm* c, Shared* sh, int rank, Conn* recvConn, Conn* sendConn, const void* sendbuff,
-                void* recvbuff, size_t esz, int datatype, const nexrDevRedOpFull& red, bool device) {
+Prims makePrims(nexrRingComm* c, Shared* sh, int rank, const void* sendbuff, void* recvbuff, size_t esz, int datatype,
+                const nexrDevRedOpFull& red, Geom g, hipStream_t stream, uint32_t* status) {
   Prims p;
   p.c = c;
   p.sh = sh;
   p.rank = rank;
-  p.recvConn = recvConn;
-  p.sendConn = sendConn;
   p.userInput = (const char*)sendbuff;
   p.userOutput = (char*)recvbuff;
   p.esz = esz;
   p.stepSize = (int64_t)(c->stepBytes / esz);
+  p.stepPerSlice = g.sliceSteps;
+  p.slicePerChunk = g.chunkSteps / g.sliceSteps;
   p.datatype = datatype;
   p.devOp = red.op;
   p.redOpArgs[0] = red.scalarArg;
   p.fn = c->cfg.fn;
   p.llFn = c->cfg.llFn;
   p.ll128Fn = c->cfg.ll128Fn;
-  p.status = c->status[rank];
-  p.stream = c->streams[rank];
-  p.device = device;
+  p.status = status;
+  p.stream = stream;
+  p.device = c->cfg.memMode == nexrRingDeviceMemory;
   return p;
 }
 
-// ncclLaunchOneRank (onerank.cc:48-83) for rank `r`'s buffers.
+// ncclLaunchOneRank (onerank.cc:48-83) for rank `r`'s buffers: every collective with nRanks == 1
+// (enqueue.cc:2354-2356).
 nexrResult_t oneRank(nexrRingComm* c, int r, const void* sendbuff, void* recvbuff, size_t count, int datatype,
                      const nexrDevRedOpFull& red, size_t esz) {
   const bool device = c->cfg.memMode == nexrRingDeviceMemory;
@@ -383,6 +605,187 @@ nexrResult_t oneRank(nexrRingComm* c, int r, const void* sendbuff, void* recvbuf
   return nexrSuccess;
 }
 
+// Common argument checks: datatype and op encoding (hostToDevRedOp, enqueue.cc:2185-2278).
+nexrResult_t prepare(nexrRingComm* c, int datatype, int op, size_t* esz, nexrDevRedOpFull* red) {
+  if (!c) return nexrInvalidArgument;
+  if (c->broken) return nexrInvalidUsage;
+  *esz = nexrTypeSize(datatype);
+  if (*esz == 0 || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
+  return nexrHostToDevRedOp(red, op, datatype, c->cfg.nRanks);
+}
+
+// Runs `jobs` (one per emulated rank, or per tree half) on host threads and collects the first error.
+nexrResult_t runThreads(nexrRingComm* c, Shared& sh, const std::vector<std::function<void()>>& jobs) {
+  std::vector<std::thread> threads;
+  threads.reserve(jobs.size());
+  for (const auto& j : jobs) threads.emplace_back(j);
+  for (auto& t : threads) t.join();
+  if (sh.firstError.load() != 0) {
+    c->broken = true;  // step counters are mid-protocol: the communicator cannot be reused
+    return (nexrResult_t)sh.firstError.load();
+  }
+  return nexrSuccess;
+}
+
+nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device) {
+  k->device = device;
+  if (c->cfg.memMode == nexrRingDeviceMemory) {
+    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, c->cfg.buffBytes) != hipSuccess)
+      return nexrUnhandledCudaError;
+  } else {
+    k->fifo = (char*)aligned_alloc(4096, c->cfg.buffBytes);
+    if (!k->fifo) return nexrSystemError;
+  }
+  return nexrSuccess;
+}
+
+nexrResult_t enablePeer(int a, int b) {
+  if (a == b) return nexrSuccess;
+  (void)hipSetDevice(a);
+  hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return nexrUnhandledCudaError;
+  (void)hipGetLastError();
+  return nexrSuccess;
+}
+
+nexrResult_t allocStatus(nexrRingComm* c, uint32_t** s) {
+  if (c->needHip) {  // pinned, device-mapped status word for the LL kernel's timeout report
+    if (hipHostMalloc((void**)s, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess) return nexrUnhandledCudaError;
+    **s = 0;
+  } else {  // CPU-side LL implementation: an ordinary host word
+    *s = (uint32_t*)calloc(1, sizeof(uint32_t));
+    if (!*s) return nexrSystemError;
+  }
+  return nexrSuccess;
+}
+
+// The tree's connections, second streams and status words, made by the first tree call.
+nexrResult_t ensureTree(nexrRingComm* c) {
+  if (!c->treeUp.empty()) return nexrSuccess;
+  const int n = c->cfg.nRanks;
+  c->treeUp.assign(n, nullptr);
+  c->treeDown.assign(n, nullptr);
+  c->streams2.assign(n, nullptr);
+  c->status2.assign(n, nullptr);
+  for (int r = 0; r < n; r++) {
+    if (c->streams[r]) {
+      if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams2[r]) != hipSuccess)
+        return nexrUnhandledCudaError;
+    }
+    if (c->ll) {
+      nexrResult_t res = allocStatus(c, &c->status2[r]);
+      if (res != nexrSuccess) return res;
+    }
+    const int up = c->tree[r].up;
+    if (up < 0) continue;
+    c->treeUp[r] = new Conn();
+    c->treeDown[r] = new Conn();
+    nexrResult_t res = allocFifo(c, c->treeUp[r], c->devices[up]);
+    if (res == nexrSuccess) res = allocFifo(c, c->treeDown[r], c->devices[r]);
+    if (res == nexrSuccess && c->cfg.memMode == nexrRingDeviceMemory) {
+      res = enablePeer(c->devices[r], c->devices[up]);
+      if (res == nexrSuccess) res = enablePeer(c->devices[up], c->devices[r]);
+    }
+    if (res != nexrSuccess) return res;
+  }
+  return nexrSuccess;
+}
+
+void freeConn(nexrRingComm* c, Conn* k) {
+  if (!k) return;
+  if (k->fifo && k->ownsFifo) {
+    if (c->cfg.memMode == nexrRingDeviceMemory) {
+      (void)hipSetDevice(k->device);
+      (void)hipFree(k->fifo);
+    } else {
+      free(k->fifo);
+    }
+  }
+  delete k;
+}
+
+bool validConfigBuff(const nexrRingComm* c) {
+  return c->cfg.buffBytes % (kSteps * 16) == 0 && c->cfg.buffBytes >= kMinBuffBytes &&
+         (c->proto != nexrRingProtoLL128 || c->cfg.buffBytes % (kSteps * 2048) == 0);  // whole LL128 slices
+}
+
+// Thread-rank collectives: the ring schedules on one thread per rank.
+enum RingColl { kAllReduce, kReduceScatter, kAllGather, kReduce, kBroadcast };
+nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* sendbuffs, void* const* recvbuffs,
+                            size_t count, int datatype, int op, int root) {
+  if (!c || c->peer) return nexrInvalidArgument;
+  size_t esz;
+  nexrDevRedOpFull red;
+  nexrResult_t r = prepare(c, datatype, op, &esz, &red);
+  if (r != nexrSuccess) return r;
+  const int n = c->cfg.nRanks;
+  if ((coll == kReduce || coll == kBroadcast) && (root < 0 || root >= n)) return nexrInvalidArgument;
+  if (!sendbuffs || !recvbuffs) return nexrInvalidArgument;
+  if (count == 0) return nexrSuccess;
+  for (int i = 0; i < n; i++) {
+    const bool needSend = coll != kBroadcast || i == root;
+    const bool needRecv = coll != kReduce || i == root;
+    if ((needSend && !sendbuffs[i]) || (needRecv && !recvbuffs[i])) return nexrInvalidArgument;
+  }
+  if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
+  const Geom g = (coll == kReduce || coll == kBroadcast) ? kGeomPipe : kGeomRing;
+  Shared sh;
+  std::vector<std::function<void()>> jobs;
+  for (int rank = 0; rank < n; rank++) {
+    jobs.emplace_back([&, rank] {
+      if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+      Prims p = makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, g, c->streams[rank],
+                          c->status[rank]);
+      p.recv[p.nRecv++] = c->conns[rank];
+      p.send[p.nSend++] = c->conns[(rank + 1) % n];
+      switch (coll) {
+        case kAllReduce: runRingAllReduce(p, n, (int64_t)count); break;
+        case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count); break;
+        case kAllGather: runRingAllGather(p, n, (int64_t)count); break;
+        case kReduce: runRingReduce(p, n, (int64_t)count, root); break;
+        case kBroadcast: runRingBroadcast(p, n, (int64_t)count, root); break;
+      }
+    });
+  }
+  return runThreads(c, sh, jobs);
+}
+
+// Process-rank collectives: this process's rank of the same ring schedules.
+nexrResult_t peerCollective(nexrRingComm* c, RingColl coll, const void* sendbuff, void* recvbuff, size_t count,
+                            int datatype, int op, int root) {
+  if (!c || !c->peer) return nexrInvalidArgument;
+  size_t esz;
+  nexrDevRedOpFull red;
+  nexrResult_t r = prepare(c, datatype, op, &esz, &red);
+  if (r != nexrSuccess) return r;
+  const int n = c->cfg.nRanks, me = c->self;
+  if ((coll == kReduce || coll == kBroadcast) && (root < 0 || root >= n)) return nexrInvalidArgument;
+  const bool needSend = coll != kBroadcast || me == root;
+  const bool needRecv = coll != kReduce || me == root;
+  if (count > 0 && ((needSend && !sendbuff) || (needRecv && !recvbuff))) return nexrInvalidArgument;
+  if (count == 0) return nexrSuccess;
+  (void)hipSetDevice(c->devices[me]);
+  if (n == 1) return oneRank(c, me, sendbuff, recvbuff, count, datatype, red, esz);
+  Shared sh;
+  sh.remoteAbort = &peerHeader(c->shm)->abort;
+  const Geom g = (coll == kReduce || coll == kBroadcast) ? kGeomPipe : kGeomRing;
+  Prims p = makePrims(c, &sh, me, sendbuff, recvbuff, esz, datatype, red, g, c->streams[me], c->status[me]);
+  p.recv[p.nRecv++] = c->conns[me];
+  p.send[p.nSend++] = c->conns[(me + 1) % n];
+  switch (coll) {
+    case kAllReduce: runRingAllReduce(p, n, (int64_t)count); break;
+    case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count); break;
+    case kAllGather: runRingAllGather(p, n, (int64_t)count); break;
+    case kReduce: runRingReduce(p, n, (int64_t)count, root); break;
+    case kBroadcast: runRingBroadcast(p, n, (int64_t)count, root); break;
+  }
+  if (sh.firstError.load() != 0) {
+    c->broken = true;
+    return (nexrResult_t)sh.firstError.load();
+  }
+  return nexrSuccess;
+}
+
 }  // namespace
 
 extern "C" {
@@ -391,6 +794,9 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024) return nexrInvalidArgument;
   if (cfg->memMode != nexrRingHostMemory && cfg->memMode != nexrRingDeviceMemory) return nexrInvalidArgument;
   if (cfg->protocol != nexrRingProtoSimple && cfg->protocol != nexrRingProtoLL && cfg->protocol != nexrRingProtoLL128)
+    return nexrInvalidArgument;
+  if (cfg->treeRanksPerNode < 0 || (cfg->treeRanksPerNode > 0 && cfg->nRanks % cfg->treeRanksPerNode != 0) ||
+      (cfg->treeIndex != 0 && cfg->treeIndex != 1))
     return nexrInvalidArgument;
   // The LL/LL128 kernels poll live FIFO lines: they need device-visible lines, i.e. device memory,
   // unless the caller supplies its own step implementation (e.g. a CPU checker).
@@ -404,8 +810,7 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   if (c->cfg.buffBytes == 0)
     c->cfg.buffBytes = c->proto == nexrRingProtoLL ? kDefaultLLBuffBytes
                        : c->proto == nexrRingProtoLL128 ? kDefaultLL128BuffBytes : kDefaultBuffBytes;
-  if (c->cfg.buffBytes % (kSteps * 16) != 0 ||
-      (c->proto == nexrRingProtoLL128 && c->cfg.buffBytes % (kSteps * 2048) != 0)) {  // whole LL128 slices
+  if (!validConfigBuff(c)) {
     delete c;
     return nexrInvalidArgument;
   }
@@ -414,67 +819,41 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   if (!c->cfg.ll128Fn) c->cfg.ll128Fn = defaultLL128Fn;
   c->stepBytes = c->cfg.buffBytes / kSteps;
   const int n = cfg->nRanks;
-  c->recvStep.assign(n, 0);
-  c->sendStep.assign(n, 0);
+  c->tree = treeTopology(n, cfg->treeRanksPerNode > 0 ? cfg->treeRanksPerNode : n, cfg->treeIndex);
   c->devices.assign(n, 0);
   c->streams.assign(n, nullptr);
   c->status.assign(n, nullptr);
   int nDev = 0;
-  const bool needHip = cfg->memMode == nexrRingDeviceMemory || (c->proto == nexrRingProtoSimple && !cfg->fn) ||
-                       (c->proto == nexrRingProtoLL && !cfg->llFn) || (c->proto == nexrRingProtoLL128 && !cfg->ll128Fn);
-  c->pinnedStatus = needHip;
-  if (needHip) {
+  c->needHip = cfg->memMode == nexrRingDeviceMemory || (c->proto == nexrRingProtoSimple && !cfg->fn) ||
+               (c->proto == nexrRingProtoLL && !cfg->llFn) || (c->proto == nexrRingProtoLL128 && !cfg->ll128Fn);
+  c->pinnedStatus = c->needHip;
+  if (c->needHip) {
     if (hipGetDeviceCount(&nDev) != hipSuccess || nDev < 1) {
       delete c;
       return nexrUnhandledCudaError;
     }
   }
+  for (int r = 0; r < n; r++) c->devices[r] = nDev > 0 ? r % nDev : 0;
   for (int r = 0; r < n; r++) {
     c->conns.push_back(new Conn());
     if (nDev > 0) {
-      c->devices[r] = r % nDev;
       if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams[r]) != hipSuccess) {
         nexrRingCommDestroy(c);
         return nexrUnhandledCudaError;
       }
     }
-    if (c->ll && needHip) {  // pinned, device-mapped status word for the LL kernel's timeout report
-      if (hipHostMalloc((void**)&c->status[r], sizeof(uint32_t), hipHostMallocMapped) != hipSuccess) {
-        nexrRingCommDestroy(c);
-        return nexrUnhandledCudaError;
-      }
-      *c->status[r] = 0;
-    } else if (c->ll) {  // CPU-side LL implementation: an ordinary host word
-      c->status[r] = (uint32_t*)calloc(1, sizeof(uint32_t));
-      if (!c->status[r]) {
-        nexrRingCommDestroy(c);
-        return nexrSystemError;
-      }
-    }
-    if (cfg->memMode == nexrRingDeviceMemory) {
-      if (hipMalloc((void**)&c->conns[r]->fifo, c->cfg.buffBytes) != hipSuccess) {
-        nexrRingCommDestroy(c);
-        return nexrUnhandledCudaError;
-      }
-    } else {
-      c->conns[r]->fifo = (char*)aligned_alloc(4096, c->cfg.buffBytes);
-      if (!c->conns[r]->fifo) {
-        nexrRingCommDestroy(c);
-        return nexrSystemError;
-      }
+    nexrResult_t res = c->ll ? allocStatus(c, &c->status[r]) : nexrSuccess;
+    if (res == nexrSuccess) res = allocFifo(c, c->conns[r], c->devices[r]);
+    if (res != nexrSuccess) {
+      nexrRingCommDestroy(c);
+      return res;
     }
   }
   if (cfg->memMode == nexrRingDeviceMemory && nDev > 1) {  // sender writes into the receiver's FIFO
     for (int r = 0; r < n; r++) {
-      int a = c->devices[r], b = c->devices[(r + 1) % n];
-      if (a != b) {
-        (void)hipSetDevice(a);
-        hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
-          nexrRingCommDestroy(c);
-          return nexrUnhandledCudaError;
-        }
-        (void)hipGetLastError();
+      if (enablePeer(c->devices[r], c->devices[(r + 1) % n]) != nexrSuccess) {
+        nexrRingCommDestroy(c);
+        return nexrUnhandledCudaError;
       }
     }
   }
@@ -484,36 +863,92 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
 
 NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op) {
-  if (!c || !sendbuffs || !recvbuffs) return nexrInvalidArgument;
-  if (c->broken) return nexrInvalidUsage;
-  const int n = c->cfg.nRanks;
-  const size_t esz = nexrTypeSize(datatype);
-  if (esz == 0 || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
+  return ringCollective(c, kAllReduce, sendbuffs, recvbuffs, count, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrRingReduceScatter(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                            size_t recvcount, int datatype, int op) {
+  return ringCollective(c, kReduceScatter, sendbuffs, recvbuffs, recvcount, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrRingAllGather(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t sendcount, int datatype) {
+  return ringCollective(c, kAllGather, sendbuffs, recvbuffs, sendcount, datatype, nexrSum, 0);  // ncclAllGather: ncclSum
+}
+
+NEXR_API nexrResult_t nexrRingReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                     size_t count, int datatype, int op, int root) {
+  return ringCollective(c, kReduce, sendbuffs, recvbuffs, count, datatype, op, root);
+}
+
+NEXR_API nexrResult_t nexrRingBroadcast(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t count, int datatype, int root) {
+  return ringCollective(c, kBroadcast, sendbuffs, recvbuffs, count, datatype, nexrSum, root);  // ncclBroadcast: ncclSum
+}
+
+NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                        size_t count, int datatype, int op) {
+  if (!c || c->peer) return nexrInvalidArgument;
+  size_t esz;
   nexrDevRedOpFull red;
-  nexrResult_t r = nexrHostToDevRedOp(&red, op, datatype, n);
+  nexrResult_t r = prepare(c, datatype, op, &esz, &red);
   if (r != nexrSuccess) return r;
-  for (int i = 0; i < n; i++)
-    if (count > 0 && (!sendbuffs[i] || !recvbuffs[i])) return nexrInvalidArgument;
+  const int n = c->cfg.nRanks;
+  if (!sendbuffs || !recvbuffs) return nexrInvalidArgument;
   if (count == 0) return nexrSuccess;
-  const bool device = c->cfg.memMode == nexrRingDeviceMemory;
-
+  for (int i = 0; i < n; i++)
+    if (!sendbuffs[i] || !recvbuffs[i]) return nexrInvalidArgument;
   if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
-
+  r = ensureTree(c);
+  if (r != nexrSuccess) {
+    c->broken = true;
+    return r;
+  }
   Shared sh;
-  std::vector<std::thread> threads;
+  std::vector<std::function<void()>> jobs;
   for (int rank = 0; rank < n; rank++) {
-    threads.emplace_back([&, rank] {
-      if (device || c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-      Prims p = makePrims(c, &sh, rank, c->conns[rank], c->conns[(rank + 1) % n], sendbuffs[rank], recvbuffs[rank],
-                          esz, datatype, red, device);
-      runRing(p, n, (int64_t)count);
+    const TreeLinks& t = c->tree[rank];
+    const bool leaf = t.down[0] == -1;
+    auto make = [&, rank](hipStream_t s, uint32_t* st) {
+      return makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, kGeomPipe, s, st);
+    };
+    if (t.up == -1) {  // root: recv from and send to every child
+      jobs.emplace_back([&, rank, make] {
+        if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+        Prims p = make(c->streams[rank], c->status[rank]);
+        const TreeLinks& tl = c->tree[rank];
+        for (int i = 0; i < tl.nDown(); i++) {
+          p.recv[p.nRecv++] = c->treeUp[tl.down[i]];
+          p.send[p.nSend++] = c->treeDown[tl.down[i]];
+        }
+        runTree(p, (int64_t)count, kTreeRoot, false);
+      });
+      continue;
+    }
+    jobs.emplace_back([&, rank, leaf, make] {  // reduce up: recv from children, send to the parent
+      if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+      Prims p = make(c->streams[rank], c->status[rank]);
+      const TreeLinks& tl = c->tree[rank];
+      for (int i = 0; i < tl.nDown(); i++) p.recv[p.nRecv++] = c->treeUp[tl.down[i]];
+      p.send[p.nSend++] = c->treeUp[rank];
+      runTree(p, (int64_t)count, kTreeReduceUp, leaf);
+    });
+    jobs.emplace_back([&, rank, leaf, make] {  // broadcast down: recv from the parent, send to children
+      if (c->streams2[rank]) (void)hipSetDevice(c->devices[rank]);
+      Prims p = make(c->streams2[rank], c->status2[rank]);
+      const TreeLinks& tl = c->tree[rank];
+      p.recv[p.nRecv++] = c->treeDown[rank];
+      for (int i = 0; i < tl.nDown(); i++) p.send[p.nSend++] = c->treeDown[tl.down[i]];
+      runTree(p, (int64_t)count, kTreeBcastDown, leaf);
     });
   }
-  for (auto& t : threads) t.join();
-  if (sh.firstError.load() != 0) {
-    c->broken = true;  // step counters are mid-protocol: the communicator cannot be reused
-    return (nexrResult_t)sh.firstError.load();
-  }
+  return runThreads(c, sh, jobs);
+}
+
+NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t c, int rank, int* up, int* down) {
+  if (!c || !up || !down || rank < 0 || rank >= c->cfg.nRanks || c->tree.empty()) return nexrInvalidArgument;
+  *up = c->tree[rank].up;
+  for (int i = 0; i < kMaxArity; i++) down[i] = c->tree[rank].down[i];
   return nexrSuccess;
 }
 
@@ -521,7 +956,9 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
   if (!c) return nexrInvalidArgument;
   if (c->peer) {
     if (!c->streams.empty() && c->streams[c->self]) (void)hipStreamSynchronize(c->streams[c->self]);
-    if (c->peerFifoIpc && c->peerFifo) (void)hipIpcCloseMemHandle(c->peerFifo);
+    const int next = (c->self + 1) % c->cfg.nRanks;
+    if (next != c->self && c->conns.size() > (size_t)next && c->conns[next]->fifo && !c->conns[next]->ownsFifo)
+      (void)hipIpcCloseMemHandle(c->conns[next]->fifo);
     if (c->shm) {
       PeerHeader* h = peerHeader(c->shm);
       // The last rank to leave removes the segment's name (each rank still unmaps its own view).
@@ -529,32 +966,25 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
       munmap(c->shm, c->shmBytes);
     }
     for (size_t r = 0; r < c->conns.size(); r++) {
-      c->conns[r]->st = &c->conns[r]->own;           // counters lived in the unmapped segment
+      c->conns[r]->st = &c->conns[r]->own;  // counters lived in the unmapped segment
       if ((int)r != c->self) c->conns[r]->fifo = nullptr;  // only this rank's FIFO is owned here
     }
   }
-  for (size_t r = 0; r < c->conns.size(); r++) {
-    Conn* k = c->conns[r];
-    if (k->fifo) {
-      if (c->cfg.memMode == nexrRingDeviceMemory) {
-        (void)hipSetDevice(c->devices[r]);
-        (void)hipFree(k->fifo);
-      } else {
-        free(k->fifo);
+  for (Conn* k : c->conns) freeConn(c, k);
+  for (Conn* k : c->treeUp) freeConn(c, k);
+  for (Conn* k : c->treeDown) freeConn(c, k);
+  for (auto* v : {&c->status, &c->status2})
+    for (uint32_t* s : *v)
+      if (s) {
+        if (c->pinnedStatus) (void)hipHostFree(s);
+        else free(s);
       }
-    }
-    delete k;
-  }
-  for (size_t r = 0; r < c->status.size(); r++)
-    if (c->status[r]) {
-      if (c->pinnedStatus) (void)hipHostFree(c->status[r]);
-      else free(c->status[r]);
-    }
-  for (size_t r = 0; r < c->streams.size(); r++)
-    if (c->streams[r]) {
-      (void)hipSetDevice(c->devices[r]);
-      (void)hipStreamDestroy(c->streams[r]);
-    }
+  for (auto* v : {&c->streams, &c->streams2})
+    for (size_t r = 0; r < v->size(); r++)
+      if ((*v)[r]) {
+        (void)hipSetDevice(c->devices[r]);
+        (void)hipStreamDestroy((*v)[r]);
+      }
   delete c;
   return nexrSuccess;
 }
@@ -586,7 +1016,7 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   if (c->cfg.buffBytes == 0)
     c->cfg.buffBytes = c->proto == nexrRingProtoLL ? kDefaultLLBuffBytes
                        : c->proto == nexrRingProtoLL128 ? kDefaultLL128BuffBytes : kDefaultBuffBytes;
-  if (c->cfg.buffBytes % (kSteps * 16) != 0 || (c->proto == nexrRingProtoLL128 && c->cfg.buffBytes % (kSteps * 2048) != 0)) {
+  if (!validConfigBuff(c)) {
     delete c;
     return nexrInvalidArgument;
   }
@@ -595,15 +1025,17 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   c->cfg.ll128Fn = defaultLL128Fn;
   c->stepBytes = c->cfg.buffBytes / kSteps;
   c->peer = true;
+  c->needHip = true;
   const int n = cfg->nRanks, me = cfg->rank, next = (me + 1) % n;
   c->self = me;
-  c->recvStep.assign(n, 0);
-  c->sendStep.assign(n, 0);
   c->devices.assign(n, cfg->device);
   c->streams.assign(n, nullptr);
   c->status.assign(n, nullptr);
   c->pinnedStatus = true;
-  for (int r = 0; r < n; r++) c->conns.push_back(new Conn());
+  for (int r = 0; r < n; r++) {
+    c->conns.push_back(new Conn());
+    c->conns[r]->device = cfg->device;
+  }
   strncpy(c->shmName, cfg->shmName, sizeof(c->shmName) - 1);
   auto fail = [&](nexrResult_t r) {
     if (c->shm) peerHeader(c->shm)->abort.store(1);
@@ -612,11 +1044,7 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   };
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreate(&c->streams[me]) != hipSuccess)
     return fail(nexrUnhandledCudaError);
-  if (c->ll) {
-    if (hipHostMalloc((void**)&c->status[me], sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
-      return fail(nexrUnhandledCudaError);
-    *c->status[me] = 0;
-  }
+  if (c->ll && allocStatus(c, &c->status[me]) != nexrSuccess) return fail(nexrUnhandledCudaError);
   // The FIFO into this rank. Uncached device memory: it is written by another process's kernels
   // (over xGMI when that process drives another GPU) between this rank's launches.
   // NEXR_PEER_FIFO_UNCACHED=0 selects ordinary (coarse-grained) device memory instead.
@@ -672,10 +1100,11 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   if (!waitFor([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t)n; })) return fail(nexrRemoteError);
   if (next != me) {
     hipIpcMemHandle_t hd = peerSlot(c->shm, next)->fifoHandle;
-    if (hipIpcOpenMemHandle((void**)&c->peerFifo, hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+    char* mapped = nullptr;
+    if (hipIpcOpenMemHandle((void**)&mapped, hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
       return fail(nexrUnhandledCudaError);
-    c->peerFifoIpc = true;
-    c->conns[next]->fifo = c->peerFifo;
+    c->conns[next]->fifo = mapped;
+    c->conns[next]->ownsFifo = false;
     c->conns[next]->st = &peerSlot(c->shm, next)->conn;
   }
   *out = c;
@@ -684,27 +1113,27 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
 
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int op) {
-  if (!c || !c->peer) return nexrInvalidArgument;
-  if (c->broken) return nexrInvalidUsage;
-  const int n = c->cfg.nRanks, me = c->self;
-  const size_t esz = nexrTypeSize(datatype);
-  if (esz == 0 || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2) return nexrInvalidArgument;
-  nexrDevRedOpFull red;
-  nexrResult_t r = nexrHostToDevRedOp(&red, op, datatype, n);
-  if (r != nexrSuccess) return r;
-  if (count > 0 && (!sendbuff || !recvbuff)) return nexrInvalidArgument;
-  if (count == 0) return nexrSuccess;
-  (void)hipSetDevice(c->devices[me]);
-  if (n == 1) return oneRank(c, me, sendbuff, recvbuff, count, datatype, red, esz);
-  Shared sh;
-  sh.remoteAbort = &peerHeader(c->shm)->abort;
-  Prims p = makePrims(c, &sh, me, c->conns[me], c->conns[(me + 1) % n], sendbuff, recvbuff, esz, datatype, red, true);
-  runRing(p, n, (int64_t)count);
-  if (sh.firstError.load() != 0) {
-    c->broken = true;
-    return (nexrResult_t)sh.firstError.load();
-  }
-  return nexrSuccess;
+  return peerCollective(c, kAllReduce, sendbuff, recvbuff, count, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrPeerRingReduceScatter(nexrRingComm_t c, const void* sendbuff, void* recvbuff,
+                                                size_t recvcount, int datatype, int op) {
+  return peerCollective(c, kReduceScatter, sendbuff, recvbuff, recvcount, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrPeerRingAllGather(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t sendcount,
+                                            int datatype) {
+  return peerCollective(c, kAllGather, sendbuff, recvbuff, sendcount, datatype, nexrSum, 0);
+}
+
+NEXR_API nexrResult_t nexrPeerRingReduce(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
+                                         int datatype, int op, int root) {
+  return peerCollective(c, kReduce, sendbuff, recvbuff, count, datatype, op, root);
+}
+
+NEXR_API nexrResult_t nexrPeerRingBroadcast(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
+                                            int datatype, int root) {
+  return peerCollective(c, kBroadcast, sendbuff, recvbuff, count, datatype, nexrSum, root);
 }
 
 }  // extern "C"

@@ -1,6 +1,7 @@
-"""Python view of the CPU-emulated ring all-reduce (include/nexr_ring.h, libnexr_ring.so).
+"""Python view of the CPU-emulated collectives (include/nexr_ring.h, libnexr_ring.so).
 
-The ring schedule (runRing, src/device/all_reduce.h:12-84) and the genericOp slicing / FIFO credit
+The ring and tree schedules (runRing of all_reduce.h, reduce_scatter.h, all_gather.h, reduce.h,
+broadcast.h; runTreeSplit, all_reduce.h:150-230) and the genericOp slicing / FIFO credit
 protocol (src/device/prims_simple.h:111-330) run on host threads in C++; every reduceCopy site calls
 the MI355X reduce-copy ABI (or any function with its signature, e.g. a test checker).
 """
@@ -14,8 +15,11 @@ from . import NexrError, Result, _check, lib
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 RING_LIB_PATH = os.path.join(_HERE, "libnexr_ring.so")
-RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
-                    "nexrPeerRingAllReduce")
+RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceScatter", "nexrRingAllGather",
+                    "nexrRingReduce", "nexrRingBroadcast", "nexrTreeAllReduce", "nexrTreeTopology",
+                    "nexrRingCommDestroy", "nexrPeerRingCommCreate", "nexrPeerRingAllReduce",
+                    "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
+                    "nexrPeerRingBroadcast")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -32,7 +36,8 @@ REDUCE_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.POINTER(cty
 class RingConfig(ctypes.Structure):
     _fields_ = [("nRanks", ctypes.c_int), ("buffBytes", ctypes.c_size_t), ("memMode", ctypes.c_int),
                 ("fn", ctypes.c_void_p), ("timeoutMs", ctypes.c_int), ("protocol", ctypes.c_int),
-                ("llFn", ctypes.c_void_p), ("ll128Fn", ctypes.c_void_p)]
+                ("llFn", ctypes.c_void_p), ("ll128Fn", ctypes.c_void_p), ("treeRanksPerNode", ctypes.c_int),
+                ("treeIndex", ctypes.c_int)]
 
 
 class PeerRingConfig(ctypes.Structure):
@@ -56,6 +61,20 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         L.nexrRingAllReduce.restype = ctypes.c_int
+        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        arr = ctypes.POINTER(ctypes.c_void_p)
+        for name, extra in (("nexrRingReduceScatter", [i32]), ("nexrRingAllGather", []), ("nexrRingReduce", [i32, i32]),
+                            ("nexrRingBroadcast", [i32]), ("nexrTreeAllReduce", [i32])):
+            f = getattr(L, name)
+            f.argtypes = [vp, arr, arr, sz, i32] + extra
+            f.restype = ctypes.c_int
+        for name, extra in (("nexrPeerRingReduceScatter", [i32]), ("nexrPeerRingAllGather", []),
+                            ("nexrPeerRingReduce", [i32, i32]), ("nexrPeerRingBroadcast", [i32])):
+            f = getattr(L, name)
+            f.argtypes = [vp, vp, vp, sz, i32] + extra
+            f.restype = ctypes.c_int
+        L.nexrTreeTopology.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.nexrTreeTopology.restype = ctypes.c_int
         L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
         L.nexrPeerRingCommCreate.restype = ctypes.c_int
         L.nexrPeerRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -68,13 +87,16 @@ def ring_lib() -> ctypes.CDLL:
 
 
 class RingComm:
-    """N emulated ranks (host threads) joined in one ring; `all_reduce` runs ncclAllReduce on all."""
+    """N emulated ranks (host threads) of one communicator: ring collectives (ncclAllReduce,
+    ncclReduceScatter, ncclAllGather, ncclReduce, ncclBroadcast) and the tree ncclAllReduce, each
+    run on all ranks at once (one buffer per rank)."""
 
     def __init__(self, n_ranks: int, mem_mode: int = HOST_MEMORY, buff_bytes: int = 0,
                  fn_address: Optional[int] = None, timeout_ms: int = 0, protocol: int = PROTO_SIMPLE,
-                 ll_fn_address: Optional[int] = None, ll128_fn_address: Optional[int] = None):
+                 ll_fn_address: Optional[int] = None, ll128_fn_address: Optional[int] = None,
+                 tree_ranks_per_node: int = 0, tree_index: int = 0):
         cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms, protocol,
-                         ll_fn_address or None, ll128_fn_address or None)
+                         ll_fn_address or None, ll128_fn_address or None, tree_ranks_per_node, tree_index)
         h = ctypes.c_void_p()
         _check(ring_lib().nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
         self._h = h
@@ -87,6 +109,42 @@ class RingComm:
         s = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in sendbuffs])
         r = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in recvbuffs])
         _check(ring_lib().nexrRingAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrRingAllReduce")
+
+    def _arrays(self, sendbuffs, recvbuffs):
+        if len(sendbuffs) != self.n_ranks or len(recvbuffs) != self.n_ranks:
+            raise NexrError(Result.InvalidArgument, "one send and one recv buffer per rank")
+        s = (ctypes.c_void_p * self.n_ranks)(*[int(p) if p else None for p in sendbuffs])
+        r = (ctypes.c_void_p * self.n_ranks)(*[int(p) if p else None for p in recvbuffs])
+        return s, r
+
+    def reduce_scatter(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingReduceScatter(self._h, s, r, int(recvcount), int(datatype), int(op)),
+               "nexrRingReduceScatter")
+
+    def all_gather(self, sendbuffs, recvbuffs, sendcount: int, datatype: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingAllGather(self._h, s, r, int(sendcount), int(datatype)), "nexrRingAllGather")
+
+    def reduce(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int, root: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingReduce(self._h, s, r, int(count), int(datatype), int(op), int(root)),
+               "nexrRingReduce")
+
+    def broadcast(self, sendbuffs, recvbuffs, count: int, datatype: int, root: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingBroadcast(self._h, s, r, int(count), int(datatype), int(root)), "nexrRingBroadcast")
+
+    def tree_all_reduce(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrTreeAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrTreeAllReduce")
+
+    def tree_topology(self, rank: int):
+        """(up, [down...]) of `rank` in this communicator's tree (-1 = none)."""
+        up = ctypes.c_int()
+        down = (ctypes.c_int * 3)()
+        _check(ring_lib().nexrTreeTopology(self._h, int(rank), ctypes.byref(up), down), "nexrTreeTopology")
+        return up.value, [d for d in down if d >= 0]
 
     def close(self) -> None:
         if self._h:
@@ -124,6 +182,22 @@ class PeerRingComm:
     def all_reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int) -> None:
         _check(ring_lib().nexrPeerRingAllReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
                                                 int(datatype), int(op)), "nexrPeerRingAllReduce")
+
+    def reduce_scatter(self, sendbuff: int, recvbuff: int, recvcount: int, datatype: int, op: int) -> None:
+        _check(ring_lib().nexrPeerRingReduceScatter(self._h, int(sendbuff) or None, int(recvbuff) or None,
+                                                    int(recvcount), int(datatype), int(op)), "nexrPeerRingReduceScatter")
+
+    def all_gather(self, sendbuff: int, recvbuff: int, sendcount: int, datatype: int) -> None:
+        _check(ring_lib().nexrPeerRingAllGather(self._h, int(sendbuff) or None, int(recvbuff) or None, int(sendcount),
+                                                int(datatype)), "nexrPeerRingAllGather")
+
+    def reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int, root: int) -> None:
+        _check(ring_lib().nexrPeerRingReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
+                                             int(datatype), int(op), int(root)), "nexrPeerRingReduce")
+
+    def broadcast(self, sendbuff: int, recvbuff: int, count: int, datatype: int, root: int) -> None:
+        _check(ring_lib().nexrPeerRingBroadcast(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
+                                                int(datatype), int(root)), "nexrPeerRingBroadcast")
 
     def close(self) -> None:
         if self._h:

@@ -1,9 +1,9 @@
-"""One rank of a process-per-rank peer ring (nexrPeerRingCommCreate / nexrPeerRingAllReduce).
+"""One rank of a process-per-rank peer ring (nexrPeerRingCommCreate / nexrPeerRing*).
 
 Started by tests/test_peer_ring_gpu.py as a child process, one per rank. Every rank regenerates
-all ranks' inputs from the seed, keeps its own, runs `calls` all-reduces on the same communicator
-(the later ones in place, so step counters carry over between calls) and saves the output of each
-call to <out>.<call>.npy.
+all ranks' inputs from the seed, keeps its own, runs `calls` collectives of kind --coll on the same
+communicator (for all-reduce the later ones in place, so step counters carry over between calls)
+and saves the output of each call to <out>.<call>.npy.
 """
 import argparse
 import importlib
@@ -23,17 +23,36 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     for name in ("rank", "n", "dt", "op", "count", "seed", "proto", "buff", "calls"):
         ap.add_argument(f"--{name}", type=int, required=True)
+    ap.add_argument("--coll", default="allreduce",
+                    choices=["allreduce", "reducescatter", "allgather", "reduce", "broadcast"])
+    ap.add_argument("--root", type=int, default=0)
     ap.add_argument("--shm", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     ring = importlib.import_module("nex-nccl_amd.ring")
-    inputs = mg.gen_inputs(a.dt, a.n, a.count, a.seed, special=True)
+    n_in = a.count * a.n if a.coll == "reducescatter" else a.count
+    n_out = a.count * a.n if a.coll == "allgather" else a.count
+    inputs = mg.gen_inputs(a.dt, a.n, n_in, a.seed, special=True)
     dev = torch.device("cuda:0")
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
-    recv = torch.zeros_like(send)
+    recv = torch.zeros(n_out, dtype=send.dtype, device=dev)
     torch.cuda.synchronize()
     with ring.PeerRingComm(a.n, a.rank, a.shm, device=0, buff_bytes=a.buff, protocol=a.proto,
                            timeout_ms=60000) as comm:
+        if a.coll != "allreduce":
+            for call in range(a.calls):
+                if a.coll == "reducescatter":
+                    comm.reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+                elif a.coll == "allgather":
+                    comm.all_gather(send.data_ptr(), recv.data_ptr(), a.count, a.dt)
+                elif a.coll == "reduce":
+                    comm.reduce(send.data_ptr(), recv.data_ptr() if a.rank == a.root else 0, a.count, a.dt, a.op,
+                                a.root)
+                else:
+                    comm.broadcast(send.data_ptr() if a.rank == a.root else 0, recv.data_ptr(), a.count, a.dt,
+                                   a.root)
+                np.save(f"{a.out}.{call}.npy", recv.cpu().numpy())
+            return 0
         comm.all_reduce(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
         np.save(f"{a.out}.0.npy", recv.cpu().numpy())
         for call in range(1, a.calls):

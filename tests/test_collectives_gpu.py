@@ -1,0 +1,124 @@
+"""GPU tests of the emulated ring collectives (reduce-scatter, all-gather, reduce, broadcast) and the
+tree all-reduce with the MI355X kernels underneath: device-memory mode (buffers and FIFOs in HBM,
+nexrReduceCopy / nexrReduceCopyLL / nexrReduceCopyLL128 per step) for every protocol, and host-memory
+mode (every step through nexrReduceCopyHost). Outputs are compared bit for bit with oracle/ring.py."""
+import importlib
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+BUFF = {0: 1 << 18, 1: 8 * 16 * 512, 2: 8 * 2048 * 8}
+PNAME = {0: "simple", 1: "ll", 2: "ll128"}
+
+
+@pytest.fixture(scope="module")
+def ring(nexr):
+    assert torch.cuda.is_available()
+    return importlib.import_module("nex-nccl_amd.ring")
+
+
+def _dev(arrs):
+    out = [torch.from_numpy(a.copy()).cuda() if a is not None else None for a in arrs]
+    torch.cuda.synchronize()
+    return out
+
+
+def _ptrs(ts):
+    return [t.data_ptr() if t is not None else 0 for t in ts]
+
+
+@pytest.mark.parametrize("proto", [0, 1, 2])
+@pytest.mark.parametrize("n,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 4), (4, mg.I32, 3), (3, mg.F16, 1)])
+def test_reduce_scatter_device(ring, oracle, proto, n, dt, op):
+    from oracle.ring import reduce_scatter_expected
+    count = 70_001
+    inputs = mg.gen_inputs(dt, n, count * n, 0x2000 + dt + op, True)
+    send = _dev(inputs)
+    recv = [torch.zeros(count, dtype=s.dtype, device=s.device) for s in send]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, BUFF[proto], protocol=proto) as comm:
+        comm.reduce_scatter(_ptrs(send), _ptrs(recv), count, dt, op)
+    exp = reduce_scatter_expected(inputs, dt, op, PNAME[proto])
+    for r in range(n):
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+@pytest.mark.parametrize("proto", [0, 1, 2])
+@pytest.mark.parametrize("in_place", [False, True])
+def test_all_gather_device(ring, oracle, proto, in_place):
+    from oracle.ring import all_gather_expected
+    n, dt, count = 3, mg.F16, 50_003
+    inputs = mg.gen_inputs(dt, n, count, 0x2100 + proto, True)
+    recv = _dev([np.zeros(count * n, dtype=inputs[0].dtype) for _ in range(n)])
+    if in_place:
+        for r in range(n):
+            recv[r][r * count:(r + 1) * count].copy_(torch.from_numpy(inputs[r]))
+        send = [recv[r][r * count:] for r in range(n)]
+    else:
+        send = _dev(inputs)
+    torch.cuda.synchronize()
+    with ring.RingComm(n, ring.DEVICE_MEMORY, BUFF[proto], protocol=proto) as comm:
+        comm.all_gather(_ptrs(send), _ptrs(recv), count, dt)
+    exp = all_gather_expected(inputs)
+    for r in range(n):
+        assert recv[r].cpu().numpy().tobytes() == exp[r].tobytes(), f"rank {r}"
+
+
+@pytest.mark.parametrize("proto", [0, 1, 2])
+@pytest.mark.parametrize("n,root,dt,op", [(3, 0, mg.F32, 0), (4, 2, mg.I8, 2), (2, 1, mg.BF16, 4)])
+def test_reduce_and_broadcast_device(ring, oracle, proto, n, root, dt, op):
+    from oracle.ring import reduce_expected, broadcast_expected
+    count = 90_007
+    inputs = mg.gen_inputs(dt, n, count, 0x2200 + root + dt, True)
+    send = _dev(inputs)
+    red = [torch.zeros_like(send[0]) if r == root else None for r in range(n)]
+    bc = [torch.zeros_like(s) for s in send]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, BUFF[proto], protocol=proto) as comm:
+        comm.reduce(_ptrs(send), _ptrs(red), count, dt, op, root)
+        comm.broadcast([send[r].data_ptr() if r == root else 0 for r in range(n)], _ptrs(bc), count, dt, root)
+    assert mg.canon_bytes(dt, red[root].cpu().numpy()) == mg.canon_bytes(dt, reduce_expected(inputs, dt, op, root,
+                                                                                            PNAME[proto]))
+    for r, e in enumerate(broadcast_expected(inputs, root)):
+        assert bc[r].cpu().numpy().tobytes() == e.tobytes(), f"rank {r}"
+
+
+@pytest.mark.parametrize("proto", [0, 1, 2])
+@pytest.mark.parametrize("n,per_node,tree_index,dt,op", [(2, 0, 0, mg.F32, 0), (5, 1, 0, mg.BF16, 0),
+                                                         (8, 2, 0, mg.F32, 0), (6, 1, 1, mg.I32, 3),
+                                                         (4, 0, 0, mg.F16, 4)])
+def test_tree_all_reduce_device(ring, oracle, proto, n, per_node, tree_index, dt, op):
+    from oracle.ring import tree_allreduce_expected, tree_topology
+    count = 120_011
+    inputs = mg.gen_inputs(dt, n, count, 0x2300 + n + per_node, True)
+    send = _dev(inputs)
+    recv = [torch.zeros_like(s) for s in send]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, BUFF[proto], protocol=proto, tree_ranks_per_node=per_node,
+                       tree_index=tree_index) as comm:
+        comm.tree_all_reduce(_ptrs(send), _ptrs(recv), count, dt, op)
+        # a second call on the same communicator, in place on the first result
+        comm.tree_all_reduce(_ptrs(recv), _ptrs(recv), count, dt, op)
+    links = tree_topology(n, per_node, tree_index)
+    exp = tree_allreduce_expected(inputs, dt, op, links, PNAME[proto])
+    exp = tree_allreduce_expected(exp, dt, op, links, PNAME[proto])
+    for r in range(n):
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+def test_host_memory_collectives_through_staging(ring, oracle):
+    # the fork's emulated transport: buffers and FIFOs in host memory, every step nexrReduceCopyHost
+    from oracle.ring import reduce_scatter_expected, tree_allreduce_expected, tree_topology
+    n, dt, op, count = 4, mg.F32, 0, 40_009
+    inputs = mg.gen_inputs(dt, n, count * n, 0x2400, False)
+    rs = [np.zeros(count, np.float32) for _ in range(n)]
+    tr = [np.zeros(count * n, np.float32) for _ in range(n)]
+    with ring.RingComm(n, ring.HOST_MEMORY, 1 << 16, tree_ranks_per_node=1) as comm:
+        comm.reduce_scatter([a.ctypes.data for a in inputs], [b.ctypes.data for b in rs], count, dt, op)
+        comm.tree_all_reduce([a.ctypes.data for a in inputs], [b.ctypes.data for b in tr], count * n, dt, op)
+    for r, e in enumerate(reduce_scatter_expected(inputs, dt, op)):
+        assert np.array_equal(rs[r].view(np.uint32), e.view(np.uint32)), f"rs rank {r}"
+    for r, e in enumerate(tree_allreduce_expected(inputs, dt, op, tree_topology(n, 1, 0))):
+        assert np.array_equal(tr[r].view(np.uint32), e.view(np.uint32)), f"tree rank {r}"

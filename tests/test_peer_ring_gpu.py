@@ -23,7 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "peer_ring_worker.py")
 
 
-def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7):
+def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="allreduce", root=0):
     name = f"/nexr_test_{uuid.uuid4().hex[:16]}"
     out = [str(tmp_path / f"rank{r}") for r in range(n)]
     procs = []
@@ -31,7 +31,7 @@ def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7):
         for r in range(n):
             cmd = [sys.executable, WORKER, "--rank", str(r), "--n", str(n), "--dt", str(dt), "--op", str(op),
                    "--count", str(count), "--seed", str(seed), "--proto", str(proto), "--buff", str(buff),
-                   "--calls", str(calls), "--shm", name, "--out", out[r]]
+                   "--calls", str(calls), "--shm", name, "--out", out[r], "--coll", coll, "--root", str(root)]
             procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
         logs = []
         for p in procs:
@@ -84,3 +84,28 @@ def test_peer_ring_c1_two_processes_fp32_sum(tmp_path):
         exp = (inputs[0] + inputs[1]).astype(np.float32)
     for r in range(2):
         assert mg.canon_bytes(mg.F32, outs[r][0]) == mg.canon_bytes(mg.F32, exp), f"rank {r}"
+
+
+@pytest.mark.parametrize("coll,n,dt,op,proto,root", [
+    ("reducescatter", 3, mg.F32, 0, 0, 0), ("reducescatter", 2, mg.BF16, 4, 1, 0), ("reducescatter", 4, mg.I32, 2, 2, 0),
+    ("allgather", 3, mg.F16, 0, 0, 0), ("allgather", 2, mg.U8, 0, 2, 0),
+    ("reduce", 3, mg.F32, 0, 0, 2), ("reduce", 4, mg.I8, 1, 1, 1),
+    ("broadcast", 3, mg.BF16, 0, 0, 1), ("broadcast", 2, mg.F64, 0, 1, 0)])
+def test_peer_ring_other_collectives(oracle, tmp_path, coll, n, dt, op, proto, root):
+    from oracle.ring import reduce_scatter_expected, all_gather_expected, reduce_expected, broadcast_expected
+    count = 100_003
+    buff = {0: 1 << 18, 1: 8 * 16 * 512, 2: 8 * 2048 * 8}[proto]
+    pname = ["simple", "ll", "ll128"][proto]
+    outs = _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, coll=coll, root=root)
+    inputs = mg.gen_inputs(dt, n, count * n if coll == "reducescatter" else count, 7, special=True)
+    if coll == "reducescatter":
+        exp = reduce_scatter_expected(inputs, dt, op, pname)
+    elif coll == "allgather":
+        exp = all_gather_expected(inputs)
+    elif coll == "reduce":
+        exp = {root: reduce_expected(inputs, dt, op, root, pname)}
+    else:
+        exp = broadcast_expected(inputs, root)
+    for r in (range(n) if coll != "reduce" else [root]):
+        for c in range(2):  # a second call on the same communicator: step counters carried over
+            assert mg.canon_bytes(dt, outs[r][c]) == mg.canon_bytes(dt, exp[r]), f"rank {r}, call {c}"
