@@ -40,20 +40,19 @@ long envLong(const char* name, long dflt) {
   return strtol(v, nullptr, 0);
 }
 
-// Grid: one workgroup per kBlock*U-pack trip ("one-shot"), capped at 2^24 workgroups beyond
+// Grid: one workgroup per kTripPacks-pack trip ("one-shot"), capped at 2^24 workgroups beyond
 // which the kernel grid-strides. Policy by the bytes the call streams (every src read once, every
 // dst written once): plain below NEXR_NT_LOAD_MIN_BYTES (64 MiB: the data likely sits in L2/MALL
 // and the consumer wants the output there too), non-temporal loads above it, non-temporal loads
 // and stores above NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3)
 // and NEXR_GRID override for sweeps.
-nexrResult_t pickGeometry(uint64_t workItems, uint64_t streamBytes, Geometry* g) {
+nexrResult_t pickGeometry(uint64_t workgroups, uint64_t streamBytes, Geometry* g) {
   static const long gridOverride = envLong("NEXR_GRID", 0);
   static const long polOverride = envLong("NEXR_POLICY", -1);
   static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);
   static const long ntStoreMin = envLong("NEXR_NT_STORE_MIN_BYTES", 512l << 20);
   const uint64_t cap = 1ull << 24;
-  uint64_t need = (workItems + kBlock - 1) / kBlock;
-  if (need < 1) need = 1;
+  uint64_t need = workgroups < 1 ? 1 : workgroups;
   g->grid = (int)(need < cap ? need : cap);
   if (gridOverride > 0) g->grid = (int)gridOverride;
   if (polOverride >= 0) g->pol = polOverride == 0 ? 0 : (polOverride == 1 ? 1 : 3);
@@ -141,9 +140,12 @@ void fillParams(RCParams& p, int nSrcs, const void* const* srcs, int nDsts, void
   planLayout(p, nSrcs, esz);
 }
 
-// Lane work items of one reduce-copy: elements (generic path) or U-pack groups (packed path).
-uint64_t workItems(const RCParams& p, int nSrcs) {
-  return p.generic ? p.nElts : (p.nPacks + unroll_for(nSrcs) - 1) / unroll_for(nSrcs);
+// One-shot workgroups of one reduce-copy: one per B lane work items, a work item being an element
+// (generic path) or a U-pack group (packed path), with (U, B) = the kernel's geometry for (dt, K).
+uint64_t workgroupsFor(const RCParams& p, int nSrcs, int dt) {
+  const uint64_t u = (uint64_t)unroll_for(dt, nSrcs), b = (uint64_t)block_for(dt, nSrcs);
+  const uint64_t items = p.generic ? p.nElts : (p.nPacks + u - 1) / u;
+  return (items + b - 1) / b;
 }
 
 hipError_t launchBatchDt(int dt, const BatchParams& b, int op, int nSrcs, int pol, int grid, hipStream_t s) {
@@ -163,7 +165,7 @@ hipError_t launchBatchDt(int dt, const BatchParams& b, int op, int nSrcs, int po
 }
 
 // One batch launch per (nSrcs, run of <= kMaxBatch works): work i gets
-// max(1, ceil(items_i / kBlock)) workgroups (its one-shot grid), total capped at 2^24 by
+// max(1, workgroupsFor(work i)) workgroups (its one-shot grid), total capped at 2^24 by
 // shrinking the largest shares (the kernel grid-strides inside each work's range).
 nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int op, hipStream_t stream) {
   if (nWorks < 0 || (nWorks > 0 && works == nullptr)) return nexrInvalidArgument;
@@ -208,7 +210,7 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
       RCParams& p = b.w[b.nWorks];
       fillParams(p, k, w.srcs, w.nDsts, w.dsts, w.nElts, esz, w.redOpArg, w.nPreOpSrcs, w.preOpArgs, nullptr,
                  w.postOp);
-      uint64_t need = (workItems(p, k) + kBlock - 1) / kBlock;
+      uint64_t need = workgroupsFor(p, k, datatype);
       blocks[b.nWorks] = need < 1 ? 1 : (need < cap ? need : cap);
       streamBytes += (uint64_t)(k + w.nDsts) * w.nElts * esz;
       if (++b.nWorks == kMaxBatch) {
@@ -232,7 +234,7 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   RCParams p;
   fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, nPreOpSrcs, preOpArgs, prePtr, postOp);
   Geometry g;
-  r = pickGeometry(workItems(p, nSrcs), (uint64_t)(nSrcs + nDsts) * nElts * esz, &g);
+  r = pickGeometry(workgroupsFor(p, nSrcs, datatype), (uint64_t)(nSrcs + nDsts) * nElts * esz, &g);
   if (r != nexrSuccess) return r;
   NEXR_HIP(launchDt(datatype, p, op, nSrcs, g, stream));
   return nexrSuccess;

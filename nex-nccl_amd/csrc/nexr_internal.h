@@ -98,10 +98,14 @@ NEXR_DECLARE_BATCH(4) NEXR_DECLARE_BATCH(5) NEXR_DECLARE_BATCH(6) NEXR_DECLARE_B
 NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 #undef NEXR_DECLARE_BATCH
 
-// Packs per lane per source in one workgroup trip (the trip covers kBlock*U packs = 16 KiB per
-// buffer). Steady-state sweeps over U in {1,2,4,8} x block in {256,512,1024} for K = 2, 4, 8
-// (tools/tune_kernel.hip, profiles/r01_tune_*.log): U = 4 with 256-thread blocks is best or
-// within noise of best for every K.
-__host__ __device__ constexpr int unroll_for(int) { return 4; }
+// Workgroup geometry per (datatype, fan-in): U packs per lane x B lanes per workgroup, always one
+// trip of kTripPacks 16-B packs (16 KiB) per buffer, so the grid is nPacks / kTripPacks either way.
+// Steady-state sweeps over U in {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8
+// (tools/tune_kernel.hip, tools/tune_sched.hip TUNE_MODE=geom; profiles/r01_tune_*.log,
+// r01_skew.log, r01s2_geom_*.log): U = 4, B = 256 is best or within noise of best everywhere except
+// fp16 with K = 8, where U = 1, B = 1024 (16 waves) is 1.7-2.8 % faster in three separate runs.
+constexpr int kTripPacks = 1024;
+__host__ __device__ constexpr int unroll_for(int dt, int k) { return dt == nexrFloat16 && k >= 8 ? 1 : 4; }
+__host__ __device__ constexpr int block_for(int dt, int k) { return kTripPacks / unroll_for(dt, k); }
 
 }  // namespace nexr

@@ -170,7 +170,7 @@ __device__ __forceinline__ void dispatch_minmax(const RCParams& p, uint64_t bid,
   }
 }
 
-template <int D, int OP, int K, int POL, int U = unroll_for(K), int B = kBlock>
+template <int D, int OP, int K, int POL, int U = unroll_for(D, K), int B = block_for(D, K)>
 __global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
   dispatch_minmax<D, OP, K, POL, U, B>(p, blockIdx.x, gridDim.x);
 }
@@ -180,10 +180,11 @@ __global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
 // owns workgroups [start[i], start[i+1]). The work index is wave-uniform, so the descriptor is read
 // straight from the kernel-argument segment with scalar loads.
 template <int D, int OP, int K, int POL>
-__global__ __launch_bounds__(kBlock) void reduce_copy_batch_kernel(BatchParams b) {
+__global__ __launch_bounds__(block_for(D, K)) void reduce_copy_batch_kernel(BatchParams b) {
   int i = 0;
   while (i + 1 < b.nWorks && blockIdx.x >= b.start[i + 1]) i++;
-  dispatch_minmax<D, OP, K, POL, unroll_for(K), kBlock>(b.w[i], blockIdx.x - b.start[i], b.start[i + 1] - b.start[i]);
+  dispatch_minmax<D, OP, K, POL, unroll_for(D, K), block_for(D, K)>(b.w[i], blockIdx.x - b.start[i],
+                                                                      b.start[i + 1] - b.start[i]);
 }
 
 template <int D, int OP, int K>
@@ -192,7 +193,7 @@ static hipError_t launch_k(const RCParams& p, const Geometry& g, hipStream_t s) 
                    : g.pol == kPolNtLoad ? (const void*)&reduce_copy_kernel<D, OP, K, kPolNtLoad>
                                          : (const void*)&reduce_copy_kernel<D, OP, K, kPolPlain>;
   void* args[] = {const_cast<RCParams*>(&p)};
-  return hipLaunchKernel(fn, dim3(g.grid), dim3(kBlock), args, 0, s);
+  return hipLaunchKernel(fn, dim3(g.grid), dim3(block_for(D, K)), args, 0, s);
 }
 
 template <int D, int OP>
@@ -216,7 +217,7 @@ static hipError_t launch_batch_k(const BatchParams& b, int pol, int grid, hipStr
                    : pol == kPolNtLoad ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNtLoad>
                                        : (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolPlain>;
   void* args[] = {const_cast<BatchParams*>(&b)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+  return hipLaunchKernel(fn, dim3(grid), dim3(block_for(D, K)), args, 0, s);
 }
 
 template <int D, int OP>

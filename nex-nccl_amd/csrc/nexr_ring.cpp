@@ -228,6 +228,17 @@ struct Prims {
 
   char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
 
+  // loadRecvConn / loadSendConn (prims_simple.h:512-513, :557-558): a SIMPLE Primitives starts each
+  // connection at step roundUp(conn->step, SlicePerChunk*StepPerSlice), so a collective with 2-step
+  // slices that follows one with 1-step slices (Broadcast, Reduce) never starts a slice in the last
+  // FIFO slot. Both endpoints of a connection hold the same step between collectives and round alike.
+  void attach() {
+    if (c->ll) return;
+    const uint64_t cs = (uint64_t)(stepPerSlice * slicePerChunk);
+    for (int i = 0; i < nRecv; i++) recv[i]->recvStep = (recv[i]->recvStep + cs - 1) / cs * cs;
+    for (int i = 0; i < nSend; i++) send[i]->sendStep = (send[i]->sendStep + cs - 1) / cs * cs;
+  }
+
   // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
   // abortable like checkAbort (primitives.h:142-156).
   bool waitAtLeast(std::atomic<uint64_t>& a, uint64_t target) {
@@ -738,6 +749,7 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
                           c->status[rank]);
       p.recv[p.nRecv++] = c->conns[rank];
       p.send[p.nSend++] = c->conns[(rank + 1) % n];
+      p.attach();
       switch (coll) {
         case kAllReduce: runRingAllReduce(p, n, (int64_t)count); break;
         case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count); break;
@@ -772,6 +784,7 @@ nexrResult_t peerCollective(nexrRingComm* c, RingColl coll, const void* sendbuff
   Prims p = makePrims(c, &sh, me, sendbuff, recvbuff, esz, datatype, red, g, c->streams[me], c->status[me]);
   p.recv[p.nRecv++] = c->conns[me];
   p.send[p.nSend++] = c->conns[(me + 1) % n];
+  p.attach();
   switch (coll) {
     case kAllReduce: runRingAllReduce(p, n, (int64_t)count); break;
     case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count); break;
@@ -921,6 +934,7 @@ NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sen
           p.recv[p.nRecv++] = c->treeUp[tl.down[i]];
           p.send[p.nSend++] = c->treeDown[tl.down[i]];
         }
+        p.attach();
         runTree(p, (int64_t)count, kTreeRoot, false);
       });
       continue;
@@ -931,6 +945,7 @@ NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sen
       const TreeLinks& tl = c->tree[rank];
       for (int i = 0; i < tl.nDown(); i++) p.recv[p.nRecv++] = c->treeUp[tl.down[i]];
       p.send[p.nSend++] = c->treeUp[rank];
+      p.attach();
       runTree(p, (int64_t)count, kTreeReduceUp, leaf);
     });
     jobs.emplace_back([&, rank, leaf, make] {  // broadcast down: recv from the parent, send to children
@@ -939,6 +954,7 @@ NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sen
       const TreeLinks& tl = c->tree[rank];
       p.recv[p.nRecv++] = c->treeDown[rank];
       for (int i = 0; i < tl.nDown(); i++) p.send[p.nSend++] = c->treeDown[tl.down[i]];
+      p.attach();
       runTree(p, (int64_t)count, kTreeBcastDown, leaf);
     });
   }

@@ -122,3 +122,32 @@ def test_host_memory_collectives_through_staging(ring, oracle):
         assert np.array_equal(rs[r].view(np.uint32), e.view(np.uint32)), f"rs rank {r}"
     for r, e in enumerate(tree_allreduce_expected(inputs, dt, op, tree_topology(n, 1, 0))):
         assert np.array_equal(tr[r].view(np.uint32), e.view(np.uint32)), f"tree rank {r}"
+
+
+def test_mixed_slice_geometries_on_one_device_comm(ring, oracle):
+    # Broadcast/Reduce move 1-step slices and can leave a connection at an odd step; the next
+    # all-reduce / reduce-scatter (2-step slices) must start at the rounded-up step
+    # (prims_simple.h:512-513, :557-558), never with a slice hanging off the FIFO's last slot.
+    from oracle.ring import broadcast_expected, ring_allreduce_expected, reduce_scatter_expected, reduce_expected
+    n, dt, buff = 3, mg.F32, 1 << 16  # 8 KiB steps
+    count = 2 * 2048 + 100            # 3 broadcast chunks: an odd step count is left on some connections
+    with ring.RingComm(n, ring.DEVICE_MEMORY, buff) as comm:
+        for it in range(3):
+            x = mg.gen_inputs(dt, n, count * n, 0x2500 + it, False)
+            send = _dev(x)
+            bc = [torch.zeros_like(s) for s in send]
+            comm.broadcast(_ptrs(send), _ptrs(bc), count + it, dt, it % n)
+            ar = [torch.zeros_like(s) for s in send]
+            comm.all_reduce(_ptrs(send), _ptrs(ar), count * n, dt, 0)
+            rs = [torch.zeros(count, dtype=s.dtype, device=s.device) for s in send]
+            comm.reduce_scatter(_ptrs(send), _ptrs(rs), count, dt, 0)
+            red = [torch.zeros_like(send[0]) if r == 1 else None for r in range(n)]
+            comm.reduce(_ptrs(send), _ptrs(red), count - it, dt, 0, 1)
+            for r, e in enumerate(broadcast_expected([v[:count + it] for v in x], it % n)):
+                assert bc[r].cpu().numpy()[:count + it].tobytes() == e.tobytes()
+            for r, e in enumerate(ring_allreduce_expected(x, dt, 0, buff)):
+                assert ar[r].cpu().numpy().tobytes() == e.tobytes()
+            for r, e in enumerate(reduce_scatter_expected(x, dt, 0)):
+                assert rs[r].cpu().numpy().tobytes() == e.tobytes()
+            e = reduce_expected([v[:count - it] for v in x], dt, 0, 1)
+            assert red[1].cpu().numpy()[:count - it].tobytes() == e.tobytes()

@@ -152,9 +152,26 @@ int main(int argc, char** argv) {
   vs.push_back({"production one-shot U4", [&](int r) {
                   reduce_copy_kernel<D, 0, K, kPolNt, 4, kBlock><<<(int)(P / 1024), kBlock>>>(ps[r]);
                 }, {}});
-  // Occupancy cap through dynamic LDS: at most `occ` workgroups (= waves per SIMD) per CU.
+  const char* mode = getenv("TUNE_MODE");
+  if (mode && strcmp(mode, "geom") == 0) {
+    // Geometry grid of the production kernel: U packs per lane x B threads per workgroup, one-shot
+    // grid, optionally capped to `occ` workgroups per CU through dynamic LDS.
+#define VG(U, B, OCC)                                                                                   \
+  {                                                                                                     \
+    const size_t lds = (OCC) ? 163840 / (OCC) - 256 : 0;                                                \
+    if (lds)                                                                                            \
+      CK(hipFuncSetAttribute((const void*)&reduce_copy_kernel<D, 0, K, kPolNt, U, B>,                    \
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 163840));                      \
+    vs.push_back({"U" #U " B" #B " occ<=" #OCC, [&, lds](int r) {                                       \
+                    reduce_copy_kernel<D, 0, K, kPolNt, U, B><<<(int)(P / ((U) * (B))), B, lds>>>(ps[r]); \
+                  }, {}});                                                                              \
+  }
+    VG(4, 256, 0) VG(4, 256, 2) VG(4, 256, 1) VG(2, 256, 0) VG(2, 512, 0) VG(2, 512, 1) VG(1, 1024, 0)
+    VG(1, 1024, 1) VG(1, 512, 0) VG(2, 1024, 0) VG(4, 512, 0) VG(4, 512, 1)
+  } else {
   CK(hipFuncSetAttribute((const void*)&reduce_copy_kernel<D, 0, K, kPolNt, 4, kBlock>,
                          hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+  // Occupancy cap through dynamic LDS: at most `occ` workgroups (= waves per SIMD) per CU.
   for (int occ : {1, 2, 3, 4, 5, 6}) {
     const size_t lds = 163840 / occ - 256;
     vs.push_back({"production one-shot U4 occ<=" + std::to_string(occ), [&, lds](int r) {
@@ -173,6 +190,7 @@ int main(int argc, char** argv) {
   VS(3, 2, nCU * 8, "persist stride pipe")
   VS(5, 2, nCU * 8, "persist xcd pipe")
   VS(5, 4, nCU * 4, "persist xcd pipe")
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
