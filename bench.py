@@ -167,6 +167,7 @@ def main(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-h2d", action="store_true")
+    ap.add_argument("--no-xgmi", action="store_true", help="skip the xGMI peer-step probe (N > 1 only)")
     ap.add_argument("--events", choices=["launch", "region"], default="region",
                     help="HIP events around every launch (default) or only around the timed region")
     args = ap.parse_args(argv)
@@ -239,6 +240,7 @@ def main(argv=None):
                    "all_cores": {"value": round(gbsN, 3), "cores": nthreads}}
         if dist.world == 1 and not args.no_h2d:
             h2d = h2d_inclusive(pkg, cfg, n)
+        xgmi = xgmi_probe() if dist.world > 1 and not args.no_xgmi else None
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -264,9 +266,26 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d,
         }
+        if xgmi is not None:
+            result["xgmi_probe"] = xgmi
         print(json.dumps(result), flush=True)
     dist.close()
     return result
+
+
+def xgmi_probe(timeout_s: float = 90.0):
+    """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, in a bounded
+    subprocess: its outcome is reported, never allowed to fail the bench line."""
+    import subprocess
+    try:
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "xgmi_probe.py")], capture_output=True,
+                           text=True, timeout=timeout_s)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        return {"error": f"exit {p.returncode}", "stderr": p.stderr[-300:]}
+    except Exception as e:  # noqa: BLE001 - reported, not raised
+        return {"error": repr(e)[:300]}
 
 
 def h2d_inclusive(pkg, cfg, n, reps: int = 3):

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""xGMI probe for the peer-memory ring step: one process, GPUs 0 and 1, peer access
+enabled both ways, and the reduce-copy kernel run on GPU 0 with one operand in GPU 1's HBM:
+
+  local        srcs = [a0, b0] -> d0          (all on GPU 0: the HBM reference)
+  remote read  srcs = [a0, b1] -> d0          (b1 streamed over xGMI into GPU 0's kernel)
+  remote write srcs = [a0, b0] -> d1          (the NCCL_P2P_WRITE pattern: the result lands in the
+                                                next GPU's memory, src/transport/p2p.cc:402)
+
+fp32 sum, 256 MiB per buffer. Prints one JSON line; with fewer than two GPUs it prints a "skipped"
+line and exits 0. bench.py runs it as a bounded subprocess when it drives more than one GPU, so a
+failure here can never take the bench line down with it.
+"""
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    import torch
+
+    n_dev = torch.cuda.device_count()
+    if n_dev < 2:
+        print(json.dumps({"skipped": f"needs 2 GPUs, found {n_dev}"}), flush=True)
+        return 0
+    if not torch.cuda.can_device_access_peer(0, 1):
+        print(json.dumps({"skipped": "GPU 0 cannot access GPU 1's memory"}), flush=True)
+        return 0
+    hip = ctypes.CDLL("libamdhip64.so")
+    for a, b in ((0, 1), (1, 0)):
+        torch.cuda.set_device(a)
+        rc = hip.hipDeviceEnablePeerAccess(ctypes.c_int(b), ctypes.c_uint(0))
+        if rc not in (0, 704):  # hipSuccess, hipErrorPeerAccessAlreadyEnabled
+            print(json.dumps({"skipped": f"hipDeviceEnablePeerAccess({a}->{b}) = {rc}"}), flush=True)
+            return 0
+    hip.hipGetLastError()
+    pkg = importlib.import_module("nex-nccl_amd")
+    pkg.lib()
+    n = 64 << 20  # fp32 elements: 256 MiB per buffer
+    torch.cuda.set_device(0)
+    d0, d1 = torch.device("cuda", 0), torch.device("cuda", 1)
+    g = torch.Generator(device=d0)
+    g.manual_seed(5)
+    a0 = torch.rand(n, device=d0, generator=g)
+    b0 = torch.rand(n, device=d0, generator=g)
+    b1 = b0.to(d1)
+    o0 = torch.empty(n, device=d0)
+    o1 = torch.empty(n, device=d1)
+    torch.cuda.synchronize(d0)
+    torch.cuda.synchronize(d1)
+    stream = torch.cuda.current_stream(d0)
+
+    def timed(srcs, dst, iters=10):
+        for _ in range(2):
+            pkg.reduce_copy_ptrs([s.data_ptr() for s in srcs], [dst.data_ptr()], n, 7, 0, 0, None, False,
+                                 stream.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(iters):
+            pkg.reduce_copy_ptrs([s.data_ptr() for s in srcs], [dst.data_ptr()], n, 7, 0, 0, None, False,
+                                 stream.cuda_stream)
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters / 1e3
+
+    buf = n * 4
+    out = {"gpus": [0, 1], "bytes_per_buffer": buf, "kernel": "nexr::reduce_copy_kernel fp32 sum K=2 M=1"}
+    t = timed([a0, b0], o0)
+    out["local"] = {"us": round(t * 1e6, 1), "alg_GBps": round(3 * buf / t / 1e9, 1)}
+    t = timed([a0, b1], o0)
+    ok_read = torch.equal(o0, a0 + b0)
+    out["remote_read"] = {"us": round(t * 1e6, 1), "xgmi_GBps": round(buf / t / 1e9, 1),
+                          "alg_GBps": round(3 * buf / t / 1e9, 1), "exact": bool(ok_read)}
+    t = timed([a0, b0], o1)
+    torch.cuda.synchronize(d1)
+    ok_write = torch.equal(o1.to(d0), a0 + b0)
+    out["remote_write"] = {"us": round(t * 1e6, 1), "xgmi_GBps": round(buf / t / 1e9, 1),
+                           "alg_GBps": round(3 * buf / t / 1e9, 1), "exact": bool(ok_write)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
