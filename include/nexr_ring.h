@@ -108,6 +108,29 @@ NEXR_API nexrResult_t nexrRingBroadcast(nexrRingComm_t comm, const void* const* 
 NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op);
 
+/* ncclReduceScatter / ncclAllGather with NCCL_ALGO_PAT, the Parallel Aggregated Trees schedules
+ * (PatRSAlgorithm / PatAGAlgorithm, src/device/collectives.h:433-906; the worker loops of
+ * reduce_scatter.h:80-139 and all_gather.h:113-172; patReduce / patCopy, prims_simple.h:992-1183).
+ * Rank r exchanges with r -/+ 2^d for every d with 2^d < nRanks; the link r -> r+1 is the ring
+ * connection, the others are made by the first PAT call. SIMPLE protocol only (nexrInvalidUsage
+ * otherwise), and, as the reference's algorithm selection (src/enqueue.cc:1779-1780), no
+ * ReduceScatter with ncclAvg (nexrInvalidArgument). Arguments as nexrRingReduceScatter /
+ * nexrRingAllGather; in-place AllGather allowed. */
+NEXR_API nexrResult_t nexrPatReduceScatter(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                           size_t recvcount, int datatype, int op);
+NEXR_API nexrResult_t nexrPatAllGather(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
+                                       size_t sendcount, int datatype);
+
+/* The PAT step stream one rank's compute thread generates for a collective of `count` elements per
+ * rank (recvcount for ReduceScatter, sendcount for AllGather), with the chunking of a communicator
+ * whose SIMPLE buffer is buffBytes (0 = 4 MiB). Writes up to capOps steps to ops[12*i ..] as
+ * {recvDim, sendDim, recvOffset, sendOffset, stepOffset, postRecv, postSend, nelem, last, skipped,
+ * inpIx, outIx} (ncclPatStep, src/device/collectives.h:407-410), the total in *nOps and the worker
+ * groups per batch in *parallelFactor. Host only: no communicator, no device. */
+NEXR_API nexrResult_t nexrPatSchedule(int reduceScatter, int nRanks, int rank, size_t count, int datatype,
+                                      size_t buffBytes, int64_t* ops, size_t capOps, size_t* nOps,
+                                      int* parallelFactor);
+
 /* The tree links of `rank` in this communicator's topology: *up (-1 at the root) and down[0..2]
  * (-1 when absent, children packed first as setTreeDown does). */
 NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t comm, int rank, int* up, int* down);

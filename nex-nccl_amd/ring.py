@@ -19,7 +19,7 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrRingReduce", "nexrRingBroadcast", "nexrTreeAllReduce", "nexrTreeTopology",
                     "nexrRingCommDestroy", "nexrPeerRingCommCreate", "nexrPeerRingAllReduce",
                     "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
-                    "nexrPeerRingBroadcast")
+                    "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -64,7 +64,8 @@ def ring_lib() -> ctypes.CDLL:
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         arr = ctypes.POINTER(ctypes.c_void_p)
         for name, extra in (("nexrRingReduceScatter", [i32]), ("nexrRingAllGather", []), ("nexrRingReduce", [i32, i32]),
-                            ("nexrRingBroadcast", [i32]), ("nexrTreeAllReduce", [i32])):
+                            ("nexrRingBroadcast", [i32]), ("nexrTreeAllReduce", [i32]),
+                            ("nexrPatReduceScatter", [i32]), ("nexrPatAllGather", [])):
             f = getattr(L, name)
             f.argtypes = [vp, arr, arr, sz, i32] + extra
             f.restype = ctypes.c_int
@@ -73,6 +74,9 @@ def ring_lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.argtypes = [vp, vp, vp, sz, i32] + extra
             f.restype = ctypes.c_int
+        L.nexrPatSchedule.argtypes = [i32, i32, i32, sz, i32, sz, ctypes.POINTER(ctypes.c_int64), sz,
+                                      ctypes.POINTER(sz), ctypes.POINTER(i32)]
+        L.nexrPatSchedule.restype = ctypes.c_int
         L.nexrTreeTopology.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.nexrTreeTopology.restype = ctypes.c_int
         L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
@@ -84,6 +88,24 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingCommDestroy.restype = ctypes.c_int
         _ring = L
     return _ring
+
+
+PAT_FIELDS = ("recvDim", "sendDim", "recvOffset", "sendOffset", "stepOffset", "postRecv", "postSend", "nelem",
+              "last", "skipped", "inpIx", "outIx")
+
+
+def pat_schedule(reduce_scatter: bool, n_ranks: int, rank: int, count: int, datatype: int, buff_bytes: int = 0):
+    """The PAT step stream of one rank (nexrPatSchedule): (list of dicts with PAT_FIELDS, parallelFactor)."""
+    L = ring_lib()
+    n_ops = ctypes.c_size_t()
+    pf = ctypes.c_int()
+    _check(L.nexrPatSchedule(int(reduce_scatter), n_ranks, rank, count, datatype, buff_bytes, None, 0,
+                             ctypes.byref(n_ops), ctypes.byref(pf)), "nexrPatSchedule")
+    buf = (ctypes.c_int64 * (12 * n_ops.value))()
+    _check(L.nexrPatSchedule(int(reduce_scatter), n_ranks, rank, count, datatype, buff_bytes, buf, n_ops.value,
+                             ctypes.byref(n_ops), ctypes.byref(pf)), "nexrPatSchedule")
+    vals = list(buf)
+    return [dict(zip(PAT_FIELDS, vals[12 * i:12 * i + 12])) for i in range(n_ops.value)], pf.value
 
 
 class RingComm:
@@ -138,6 +160,17 @@ class RingComm:
     def tree_all_reduce(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
         _check(ring_lib().nexrTreeAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrTreeAllReduce")
+
+    def pat_reduce_scatter(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
+        """ncclReduceScatter with NCCL_ALGO_PAT (SIMPLE)."""
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrPatReduceScatter(self._h, s, r, int(recvcount), int(datatype), int(op)),
+               "nexrPatReduceScatter")
+
+    def pat_all_gather(self, sendbuffs, recvbuffs, sendcount: int, datatype: int) -> None:
+        """ncclAllGather with NCCL_ALGO_PAT (SIMPLE)."""
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrPatAllGather(self._h, s, r, int(sendcount), int(datatype)), "nexrPatAllGather")
 
     def tree_topology(self, rank: int):
         """(up, [down...]) of `rank` in this communicator's tree (-1 = none)."""

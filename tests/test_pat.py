@@ -1,0 +1,204 @@
+"""CPU tests of the PAT ReduceScatter / AllGather (NCCL_ALGO_PAT; include/nexr_ring.h nexrPat*).
+
+Three layers, each against oracle/pat.py (a restatement of the reference's PatRSAlgorithm /
+PatAGAlgorithm, src/device/collectives.h:433-906, run on an idealised machine without FIFO limits):
+  - the step stream the C++ generators produce (nexrPatSchedule) equals the restatement's, op for op;
+  - the emulated collectives (host threads, 8-slot FIFOs with credits, the oracle serving every
+    reduceCopy) give the restatement's results bit for bit, including FIFO wrap-around, aggregated
+    steps (postFreq > 1) and step offsets;
+  - integer sums agree with a plain numpy reduction (fold order cannot matter for wrapping ints).
+"""
+import ctypes
+import importlib
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+
+@pytest.fixture(scope="module")
+def ring(nexr):
+    return importlib.import_module("nex-nccl_amd.ring")
+
+
+@pytest.fixture(scope="module")
+def fn(oracle):
+    return ctypes.cast(oracle.lib().oracle_reduce_copy_fn, ctypes.c_void_p).value
+
+
+def _ptrs(arrs):
+    return [a.ctypes.data if a is not None else 0 for a in arrs]
+
+
+def _comm(ring, fn, n, buff, proto=0):
+    return ring.RingComm(n, ring.HOST_MEMORY, buff, fn, 20000, proto)
+
+
+@pytest.mark.parametrize("reduce_scatter", [True, False])
+def test_schedule_matches_restatement(ring, reduce_scatter):
+    from oracle import pat
+    for n in list(range(2, 18)) + [31, 32, 33, 64]:
+        for count in (1, 5, 100, 1000, 3001, 70_000):
+            for buff, dt, esz in ((4096, mg.F32, 4), (64 << 10, mg.F16, 2), (4 << 20, mg.F32, 4), (1 << 20, mg.I8, 1)):
+                for r in sorted({0, 1, n // 2, n - 1}):
+                    got, pf = ring.pat_schedule(reduce_scatter, n, r, count, dt, buff)
+                    exp, pf_exp = pat.schedule(reduce_scatter, n, r, count, esz, buff // 8)
+                    assert pf == pf_exp and got == exp, (n, count, buff, r)
+                    # the worker groups end together: whole batches, the last one all marked
+                    assert len(got) % pf == 0 and all(op["last"] for op in got[-pf:])
+                    assert not any(op["last"] for op in got[:-pf])
+
+
+def test_schedule_geometry_properties(ring):
+    """Every FIFO access stays inside one step, stepOffsets stay below NCCL_STEPS, and each rank's
+    ReduceScatter output is produced exactly once per chunk (the phase-4 step)."""
+    for n in (2, 3, 5, 8, 16, 24):
+        for count in (3, 700, 5000):
+            buff = 16 << 10
+            step_elems = buff // 8 // 4
+            ops, pf = ring.pat_schedule(True, n, 0, count, mg.F32, buff)
+            final = [op for op in ops if not op["skipped"] and op["sendDim"] < 0]
+            assert sum(op["nelem"] for op in final if op["recvDim"] == 0) == count
+            for kind in (True, False):
+                ops, pf = ring.pat_schedule(kind, n, n - 1, count, mg.F32, buff)
+                for op in ops:
+                    if op["skipped"]:
+                        continue
+                    assert 0 <= op["stepOffset"] < 8
+                    for off in (op["recvOffset"], op["sendOffset"]):
+                        if off >= 0:
+                            assert off + op["nelem"] <= step_elems
+
+
+CASES = [(mg.F32, 0, False), (mg.BF16, 0, True), (mg.F16, 1, True), (mg.I32, 2, True), (mg.I8, 3, True),
+         (mg.U64, 0, True), (mg.F64, 2, False)]
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3, 4, 5, 8, 13])
+@pytest.mark.parametrize("dt,op,special", CASES)
+def test_pat_reduce_scatter(ring, oracle, fn, n_ranks, dt, op, special):
+    from oracle import pat
+    buff = 8 * 1024  # 1 KiB steps: many chunks, FIFO wrap
+    for recvcount in (1, 77, 4_001):
+        inputs = mg.gen_inputs(dt, n_ranks, recvcount * n_ranks, 0x9A7 + 11 * dt + op + recvcount, special)
+        recv = [np.zeros_like(x[:recvcount]) for x in inputs]
+        with _comm(ring, fn, n_ranks, buff) as comm:
+            comm.pat_reduce_scatter(_ptrs(inputs), _ptrs(recv), recvcount, dt, op)
+        dev_op, arg = oracle.host_to_dev_red_op(op, dt, n_ranks)
+        exp = pat.reduce_scatter_expected(inputs, dt, dev_op, arg, buff // 8)
+        for r in range(n_ranks):
+            assert mg.canon_bytes(dt, recv[r]) == mg.canon_bytes(dt, exp[r]), (recvcount, r)
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3, 6, 8, 16, 17])
+def test_pat_reduce_scatter_int_sum_matches_numpy(ring, fn, n_ranks):
+    recvcount = 3_333
+    inputs = mg.gen_inputs(mg.I32, n_ranks, recvcount * n_ranks, 0x51 + n_ranks, False)
+    recv = [np.zeros(recvcount, dtype=inputs[0].dtype) for _ in range(n_ranks)]
+    with _comm(ring, fn, n_ranks, 4096) as comm:
+        comm.pat_reduce_scatter(_ptrs(inputs), _ptrs(recv), recvcount, mg.I32, 0)
+    total = np.zeros(recvcount * n_ranks, dtype=np.uint64)
+    for x in inputs:
+        total += x.view(np.uint32).astype(np.uint64)
+    total = (total & 0xFFFFFFFF).astype(np.uint32)
+    for r in range(n_ranks):
+        assert np.array_equal(recv[r].view(np.uint32), total[r * recvcount:(r + 1) * recvcount]), r
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3, 4, 7, 8, 16])
+@pytest.mark.parametrize("in_place", [False, True])
+def test_pat_all_gather(ring, fn, n_ranks, in_place):
+    from oracle import pat
+    dt = mg.F16
+    buff = 8 * 1024
+    for count in (1, 300, 6_007):
+        inputs = mg.gen_inputs(dt, n_ranks, count, 0xA6 + n_ranks + count, True)  # NaN payloads survive copies
+        recv = [np.zeros(count * n_ranks, dtype=inputs[0].dtype) for _ in range(n_ranks)]
+        if in_place:
+            for r in range(n_ranks):
+                recv[r][r * count:(r + 1) * count] = inputs[r]
+            send = [recv[r][r * count:] for r in range(n_ranks)]
+        else:
+            send = inputs
+        with _comm(ring, fn, n_ranks, buff) as comm:
+            comm.pat_all_gather(_ptrs(send), _ptrs(recv), count, dt)
+        exp = np.concatenate(inputs)
+        sim = pat.all_gather_expected(inputs, buff // 8)
+        for r in range(n_ranks):
+            assert recv[r].tobytes() == exp.tobytes() == sim[r].tobytes(), (count, r)
+
+
+@pytest.mark.parametrize("n,count,buff", [(16, 40, 4 << 20), (32, 40, 64 << 10), (32, 1000, 4096), (64, 1000, 4096)])
+def test_pat_aggregation_and_step_offsets(ring, oracle, fn, n, count, buff):
+    """Small per-rank counts make several chunks share one FIFO step (postFreq > 1, several worker
+    groups per batch); with more ranks the generators keep several steps in flight per peer
+    (stepOffset > 0, up to NCCL_STEPS-1 at 64 ranks)."""
+    from oracle import pat
+    feats = set()
+    for rs in (True, False):
+        ops, pf = ring.pat_schedule(rs, n, 0, count, mg.F32, buff)
+        feats |= {"pf"} if pf > 1 else set()
+        feats |= {"offset"} if any(op["stepOffset"] > 0 for op in ops) else set()
+    assert feats, "configuration exercises neither aggregation nor step offsets"
+    for dt, op in ((mg.F32, 0), (mg.BF16, 0), (mg.I8, 1)):
+        inputs = mg.gen_inputs(dt, n, count * n, 0x77 + dt + n, True)
+        recv = [np.zeros_like(x[:count]) for x in inputs]
+        ag = [np.zeros_like(inputs[0]) for _ in range(n)]
+        with _comm(ring, fn, n, buff) as comm:
+            comm.pat_reduce_scatter(_ptrs(inputs), _ptrs(recv), count, dt, op)
+            comm.pat_all_gather(_ptrs([x[:count] for x in inputs]), _ptrs(ag), count, dt)
+        dev_op, arg = oracle.host_to_dev_red_op(op, dt, n)
+        exp = pat.reduce_scatter_expected(inputs, dt, dev_op, arg, buff // 8)
+        gathered = np.concatenate([x[:count] for x in inputs]).tobytes()
+        for r in range(n):
+            assert mg.canon_bytes(dt, recv[r]) == mg.canon_bytes(dt, exp[r]), r
+            assert ag[r].tobytes() == gathered, r
+
+
+def test_pat_and_ring_share_one_comm(ring, oracle, fn):
+    """PAT's r -> r+1 link is the ring connection: ring and PAT collectives interleave on one
+    communicator with their step counters carried across calls."""
+    from oracle import pat
+    from oracle.ring import reduce_scatter_expected, ring_allreduce_expected
+    n, buff = 4, 8 * 1024
+    with _comm(ring, fn, n, buff) as comm:
+        for it in range(3):
+            x = mg.gen_inputs(mg.F32, n, n * 2_000, 0x300 + it, False)
+            out = [np.zeros(2_000, np.float32) for _ in range(n)]
+            comm.pat_reduce_scatter(_ptrs(x), _ptrs(out), 2_000, mg.F32, 0)
+            for r, e in enumerate(pat.reduce_scatter_expected(x, mg.F32, 0, 0, buff // 8)):
+                assert out[r].tobytes() == e.tobytes()
+            comm.reduce_scatter(_ptrs(x), _ptrs(out), 2_000, mg.F32, 0)
+            for r, e in enumerate(reduce_scatter_expected(x, mg.F32, 0)):
+                assert out[r].tobytes() == e.tobytes()
+            ar = [np.zeros_like(v) for v in x]
+            comm.all_reduce(_ptrs(x), _ptrs(ar), x[0].size, mg.F32, 0)
+            for r, e in enumerate(ring_allreduce_expected(x, mg.F32, 0, buff)):
+                assert ar[r].tobytes() == e.tobytes()
+            ag = [np.zeros(n * 2_000, np.float32) for _ in range(n)]
+            comm.pat_all_gather(_ptrs(out), _ptrs(ag), 2_000, mg.F32)
+            for r in range(n):
+                assert ag[r].tobytes() == np.concatenate(out).tobytes()
+
+
+def test_pat_one_rank_empty_and_rejections(ring, fn, nexr):
+    x = mg.gen_inputs(mg.F32, 1, 1000, 9, False)[0]
+    out = np.zeros_like(x)
+    with _comm(ring, fn, 1, 8192) as comm:
+        comm.pat_all_gather(_ptrs([x]), _ptrs([out]), 1000, mg.F32)
+        assert out.tobytes() == x.tobytes()
+    a = np.zeros(3 * 64, np.float32)
+    with _comm(ring, fn, 3, 8192) as comm:
+        comm.pat_reduce_scatter(_ptrs([a] * 3), _ptrs([a] * 3), 0, mg.F32, 0)  # empty: no-op
+        with pytest.raises(nexr.NexrError) as e:
+            comm.pat_reduce_scatter(_ptrs([a] * 3), _ptrs([a] * 3), 64, mg.F32, 4)  # ncclAvg: no PAT
+        assert e.value.code == nexr.Result.InvalidArgument
+        with pytest.raises(nexr.NexrError):
+            comm.pat_all_gather(_ptrs([a] * 3), [a.ctypes.data, 0, a.ctypes.data], 64, mg.F32)
+    with ring.RingComm(2, ring.HOST_MEMORY, 8 * 1024, fn, 20000, ring.PROTO_LL, fn, fn) as comm:
+        with pytest.raises(nexr.NexrError) as e:
+            comm.pat_all_gather(_ptrs([a] * 2), _ptrs([a] * 2), 32, mg.F32)  # SIMPLE only
+        assert e.value.code == nexr.Result.InvalidUsage
+    with pytest.raises(nexr.NexrError):
+        ring.pat_schedule(True, 1, 0, 10, mg.F32)

@@ -28,7 +28,7 @@ def run(n, mode_name, proto_name, coll, iters):
     rng = np.random.default_rng(n)
     # small integers: every sum order gives the same fp32 result, so numpy checks the schedule
     x = [rng.integers(-1000, 1000, count * n).astype(np.float32) for _ in range(n)]
-    out_n = count * n if coll == "allgather" else count
+    out_n = count * n if coll in ("allgather", "pat_ag") else count
     if mode == ring.DEVICE_MEMORY:
         send = [torch.from_numpy(v).cuda() for v in x]
         recv = [torch.zeros(out_n, dtype=torch.float32, device="cuda") for _ in range(n)]
@@ -43,7 +43,9 @@ def run(n, mode_name, proto_name, coll, iters):
         call = {"allreduce": lambda: comm.all_reduce(sp, rp, count, F32, 0),
                 "tree": lambda: comm.tree_all_reduce(sp, rp, count, F32, 0),
                 "reducescatter": lambda: comm.reduce_scatter(sp, rp, count, F32, 0),
-                "allgather": lambda: comm.all_gather(sp, rp, count, F32)}[coll]
+                "allgather": lambda: comm.all_gather(sp, rp, count, F32),
+                "pat_rs": lambda: comm.pat_reduce_scatter(sp, rp, count, F32, 0),
+                "pat_ag": lambda: comm.pat_all_gather(sp, rp, count, F32)}[coll]
         call()
         t0 = time.perf_counter()
         for _ in range(iters):
@@ -52,7 +54,7 @@ def run(n, mode_name, proto_name, coll, iters):
     got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
     if coll in ("allreduce", "tree"):
         exp = [sum(v[:count] for v in x)] * n
-    elif coll == "reducescatter":
+    elif coll in ("reducescatter", "pat_rs"):
         exp = [sum(v[k * count:(k + 1) * count] for v in x) for k in range(n)]
     else:
         exp = [np.concatenate([v[:count] for v in x])] * n
@@ -61,11 +63,12 @@ def run(n, mode_name, proto_name, coll, iters):
 
 
 print(f"{'ranks':>5} {'mode':<10} {'proto':<6} {'collective':<14} {'ms/call':>9} {'algbw GB/s':>11}")
-for n in (2, 4):
+for n in [int(v) for v in os.environ.get("RING_TIME_RANKS", "2,4").split(",")]:
     for mode_name, protos in (("cpu-oracle", ("simple",)), ("host", ("simple",)),
                               ("device", ("simple", "ll", "ll128"))):
         for proto_name in protos:
-            for coll in ("allreduce", "tree", "reducescatter", "allgather"):
+            colls = ("allreduce", "tree", "reducescatter", "allgather")
+            for coll in colls + (("pat_rs", "pat_ag") if proto_name == "simple" else ()):
                 iters = 3 if mode_name == "cpu-oracle" else 10
                 dt = run(n, mode_name, proto_name, coll, iters)
                 print(f"{n:>5} {mode_name:<10} {proto_name:<6} {coll:<14} {dt * 1e3:9.3f} {count * 4 / dt / 1e9:11.2f}",
