@@ -121,6 +121,17 @@ NEXR_API nexrResult_t nexrPatReduceScatter(nexrRingComm_t comm, const void* cons
 NEXR_API nexrResult_t nexrPatAllGather(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
                                        size_t sendcount, int datatype);
 
+/* ncclSend / ncclRecv issued by every rank inside one ncclGroupStart/End (the P2P work batch,
+ * src/device/sendrecv.h): rank r sends `bytes` bytes of sendbuffs[r] to rank sendPeers[r] and
+ * receives `bytes` bytes from rank recvPeers[r] into recvbuffs[r] (-1: no send / no recv). Every
+ * send must meet the matching recv (recvPeers[sendPeers[r]] == r), else nexrInvalidArgument. A
+ * rank's send and recv run concurrently on its two streams over connection-index-1 FIFOs with
+ * 8 steps of the P2P chunk size (128 KiB, at most buffBytes/8); a send to self is one copy.
+ * SIMPLE protocol only: the reference's LL path for messages <= 16 KiB (enqueue.cc:786-839) is not
+ * restated (nexrInvalidUsage on an LL/LL128 communicator). */
+NEXR_API nexrResult_t nexrSendRecv(nexrRingComm_t comm, const void* const* sendbuffs, const int* sendPeers,
+                                   void* const* recvbuffs, const int* recvPeers, size_t bytes);
+
 /* The PAT step stream one rank's compute thread generates for a collective of `count` elements per
  * rank (recvcount for ReduceScatter, sendcount for AllGather), with the chunking of a communicator
  * whose SIMPLE buffer is buffBytes (0 = 4 MiB). Writes up to capOps steps to ops[12*i ..] as

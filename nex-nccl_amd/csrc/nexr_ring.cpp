@@ -45,6 +45,7 @@ struct ConnState {
 };
 struct Conn {
   char* fifo = nullptr;
+  size_t slotBytes = 0;  // bytes per FIFO step; 0 = the communicator's stepBytes (P2P links: p2pChunkSize)
   int device = 0;        // device of the FIFO (device memory mode)
   bool ownsFifo = true;  // false for a peer process's FIFO mapped over IPC
   ConnState own;
@@ -168,6 +169,8 @@ struct nexrRingComm {
   std::vector<Conn*> treeUp;    // treeUp[r]: r -> parent(r) (reduce); created by the first tree call
   std::vector<Conn*> treeDown;  // treeDown[r]: parent(r) -> r (broadcast)
   std::vector<Conn*> patConns;  // PAT: patConns[from*nRanks+to] for to = from +- 2^d (ring link excluded)
+  std::vector<Conn*> p2pConns;  // ncclSend/ncclRecv: p2pConns[from*nRanks+to] (connIndex 1), made on first use
+  size_t p2pChunkBytes = 0;     // comm->p2pChunkSize
   std::vector<int> devices;
   std::vector<hipStream_t> streams, streams2;  // streams2: the tree's broadcast-half threads
   std::vector<uint32_t*> status, status2;      // LL: pinned status words the kernel reports timeouts in
@@ -228,6 +231,7 @@ struct Prims {
   bool device;
 
   char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
+  size_t slot(const Conn* q) const { return q->slotBytes ? q->slotBytes : c->stepBytes; }
 
   // loadRecvConn / loadSendConn (prims_simple.h:512-513, :557-558): a SIMPLE Primitives starts each
   // connection at step roundUp(conn->step, SlicePerChunk*StepPerSlice), so a collective with 2-step
@@ -282,14 +286,14 @@ struct Prims {
       for (int i = 0; i < nr; i++) {  // wait for the peer's data: tail >= step + StepPerSlice
         Conn* q = recv[i];
         if (!waitAtLeast(q->st->tail, q->recvStep + stepPerSlice)) return false;
-        srcs[k++] = q->fifo + (q->recvStep % kSteps) * c->stepBytes;
+        srcs[k++] = q->fifo + (q->recvStep % kSteps) * slot(q);
       }
       for (int i = 0; i < ns; i++) {  // wait for credit: head + NCCL_STEPS >= step + StepPerSlice
         Conn* q = send[i];
         if (q->sendStep + stepPerSlice > (uint64_t)kSteps &&
             !waitAtLeast(q->st->head, q->sendStep + stepPerSlice - kSteps))
           return false;
-        dsts[m++] = q->fifo + (q->sendStep % kSteps) * c->stepBytes;
+        dsts[m++] = q->fifo + (q->sendStep % kSteps) * slot(q);
       }
       if (sliceSize > 0 && k > 0 && m > 0) {
         // PreOpSrcs = SrcBuf != Input ? 0 : 1 (prims_simple.h:279-280); preOpArgs = redOpArgs.
@@ -671,12 +675,11 @@ nexrResult_t allocStatus(nexrRingComm* c, uint32_t** s) {
   return nexrSuccess;
 }
 
-// The tree's connections, second streams and status words, made by the first tree call.
-nexrResult_t ensureTree(nexrRingComm* c) {
-  if (!c->treeUp.empty()) return nexrSuccess;
+// A second stream and status word per rank, for ranks that run two halves at once (the tree's
+// reduce-up / broadcast-down, a send beside a recv).
+nexrResult_t ensureSecondStreams(nexrRingComm* c) {
+  if (!c->streams2.empty()) return nexrSuccess;
   const int n = c->cfg.nRanks;
-  c->treeUp.assign(n, nullptr);
-  c->treeDown.assign(n, nullptr);
   c->streams2.assign(n, nullptr);
   c->status2.assign(n, nullptr);
   for (int r = 0; r < n; r++) {
@@ -688,6 +691,19 @@ nexrResult_t ensureTree(nexrRingComm* c) {
       nexrResult_t res = allocStatus(c, &c->status2[r]);
       if (res != nexrSuccess) return res;
     }
+  }
+  return nexrSuccess;
+}
+
+// The tree's connections (and the second streams), made by the first tree call.
+nexrResult_t ensureTree(nexrRingComm* c) {
+  if (!c->treeUp.empty()) return nexrSuccess;
+  const int n = c->cfg.nRanks;
+  c->treeUp.assign(n, nullptr);
+  c->treeDown.assign(n, nullptr);
+  nexrResult_t sres = ensureSecondStreams(c);
+  if (sres != nexrSuccess) return sres;
+  for (int r = 0; r < n; r++) {
     const int up = c->tree[r].up;
     if (up < 0) continue;
     c->treeUp[r] = new Conn();
@@ -1401,6 +1417,118 @@ nexrResult_t patCollective(nexrRingComm* c, bool reduceScatter, const void* cons
   return runThreads(c, sh, jobs);
 }
 
+// ---- ncclSend / ncclRecv (the P2P work batch, src/device/sendrecv.h) --------------------------------
+// Every rank's send and recv run side by side, as the reference splits a work's warps between
+// them (sendrecv.h:144-176): the send half on the rank's stream, the recv half on its second stream.
+// runSend / runRecv (:15-62) move the message in chunks of the P2P chunk size through
+// Primitives<FanAsymmetric<0,1> / <1,0>, ProtoSimple<1,1>> on connection index 1: directSend is
+// genericOp(Input -> peer FIFO) and directRecv genericOp(peer FIFO -> Output). A send to self is one
+// reduceCopy copy (:192-194). Messages are bytes (T = int8, :13).
+
+// u32fp8Encode/Decode (src/include/bitops.h:384-410): the work descriptor carries the chunk size in
+// 8 bits, so the chunk the kernels use is the encoded value decoded again (enqueue.cc:854-855).
+uint32_t u32fp8RoundTrip(uint32_t x) {
+  const int log2x = 31 - __builtin_clz(x | 1);
+  const uint32_t mant = x >> (log2x >= 3 ? log2x - 3 : 0) & 7u;
+  uint32_t expo = log2x >= 3 ? (uint32_t)(log2x - 2) : 0;
+  const uint32_t m = mant | (expo != 0 ? 8u : 0u);
+  if (expo != 0) expo -= 1;
+  return m << expo;
+}
+
+Conn* p2pConn(nexrRingComm* c, int from, int to) { return c->p2pConns[(size_t)from * c->cfg.nRanks + to]; }
+
+nexrResult_t ensureP2p(nexrRingComm* c, const int* sendPeers) {
+  const int n = c->cfg.nRanks;
+  if (c->p2pConns.empty()) c->p2pConns.assign((size_t)n * n, nullptr);
+  for (int r = 0; r < n; r++) {
+    const int q = sendPeers[r];
+    if (q < 0 || q == r || p2pConn(c, r, q)) continue;
+    Conn* k = new Conn();
+    c->p2pConns[(size_t)r * n + q] = k;
+    k->slotBytes = c->p2pChunkBytes;
+    nexrResult_t res = allocFifo(c, k, c->devices[q]);
+    if (res == nexrSuccess && c->cfg.memMode == nexrRingDeviceMemory) res = enablePeer(c->devices[r], c->devices[q]);
+    if (res != nexrSuccess) return res;
+  }
+  return nexrSuccess;
+}
+
+nexrResult_t sendRecv(nexrRingComm* c, const void* const* sendbuffs, const int* sendPeers, void* const* recvbuffs,
+                      const int* recvPeers, size_t bytes) {
+  if (!c || c->peer || !sendbuffs || !sendPeers || !recvbuffs || !recvPeers) return nexrInvalidArgument;
+  if (c->broken) return nexrInvalidUsage;
+  if (c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
+  const int n = c->cfg.nRanks;
+  for (int r = 0; r < n; r++) {  // every send matches the peer's recv, and the other way round
+    const int s = sendPeers[r], v = recvPeers[r];
+    if (s < -1 || s >= n || v < -1 || v >= n) return nexrInvalidArgument;
+    if (s >= 0 && recvPeers[s] != r) return nexrInvalidArgument;
+    if (v >= 0 && sendPeers[v] != r) return nexrInvalidArgument;
+    if (bytes > 0 && ((s >= 0 && !sendbuffs[r]) || (v >= 0 && !recvbuffs[r]))) return nexrInvalidArgument;
+  }
+  if (bytes == 0) return nexrSuccess;
+  nexrResult_t res = ensureSecondStreams(c);
+  if (res == nexrSuccess) res = ensureP2p(c, sendPeers);
+  if (res != nexrSuccess) {
+    c->broken = true;
+    return res;
+  }
+  const int64_t chunk = (int64_t)u32fp8RoundTrip((uint32_t)c->p2pChunkBytes);
+  const nexrDevRedOpFull copy = {nexrDevSum, 0, 0, 0};
+  Shared sh;
+  std::vector<std::function<void()>> jobs;
+  for (int rank = 0; rank < n; rank++) {
+    const int to = sendPeers[rank], from = recvPeers[rank];
+    if (to == rank) {  // isCopy: one reduceCopy from the send buffer to the recv buffer
+      jobs.emplace_back([&, rank] {
+        if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+        const void* src = sendbuffs[rank];
+        void* dst = recvbuffs[rank];
+        nexrResult_t r = c->cfg.fn(1, &src, 1, &dst, bytes, nexrInt8, nexrDevSum, 0, 0, nullptr, 0,
+                                   (nexrStream_t)c->streams[rank]);
+        if (r == nexrSuccess && c->streams[rank] && c->cfg.memMode == nexrRingDeviceMemory &&
+            hipStreamSynchronize(c->streams[rank]) != hipSuccess)
+          r = nexrUnhandledCudaError;
+        if (r != nexrSuccess) sh.fail(r);
+      });
+      continue;
+    }
+    auto make = [&, rank](hipStream_t s) {
+      Prims p = makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], 1, nexrInt8, copy, kGeomPipe, s, nullptr);
+      p.stepSize = (int64_t)c->p2pChunkBytes;  // Primitives' P2P stepSize argument (sendrecv.h:27-29)
+      return p;
+    };
+    if (to >= 0) {
+      jobs.emplace_back([&, rank, to, make] {  // runSend
+        if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+        Prims p = make(c->streams[rank]);
+        p.send[p.nSend++] = p2pConn(c, rank, to);
+        p.attach();
+        for (int64_t cursor = 0; cursor < (int64_t)bytes;) {
+          const int64_t m = std::min<int64_t>(chunk, (int64_t)bytes - cursor);
+          if (!p.sendInput(cursor, m)) return;
+          cursor += m;
+        }
+      });
+    }
+    if (from >= 0) {
+      jobs.emplace_back([&, rank, from, make] {  // runRecv
+        if (c->streams2[rank]) (void)hipSetDevice(c->devices[rank]);
+        Prims p = make(c->streams2[rank]);
+        p.recv[p.nRecv++] = p2pConn(c, from, rank);
+        p.attach();
+        for (int64_t cursor = 0; cursor < (int64_t)bytes;) {
+          const int64_t m = std::min<int64_t>(chunk, (int64_t)bytes - cursor);
+          if (!p.recvOutput(cursor, m)) return;
+          cursor += m;
+        }
+      });
+    }
+  }
+  return runThreads(c, sh, jobs);
+}
+
 // The op stream of one rank, as plain ints for inspection: 12 per op, in the order of PatOp's fields
 // recvDim, sendDim, recvOffset, sendOffset, stepOffset, postRecv, postSend, nelem, last, skipped,
 // inpIx, outIx.
@@ -1461,6 +1589,9 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   if (!c->cfg.llFn) c->cfg.llFn = defaultLLFn;
   if (!c->cfg.ll128Fn) c->cfg.ll128Fn = defaultLL128Fn;
   c->stepBytes = c->cfg.buffBytes / kSteps;
+  // comm->p2pChunkSize (init.cc:637-642): NCCL_P2P_PCI_CHUNKSIZE (128 KiB, the single-node non-NVLink
+  // default), at most one SIMPLE step.
+  c->p2pChunkBytes = std::min<size_t>(128 << 10, c->stepBytes);
   const int n = cfg->nRanks;
   c->tree = treeTopology(n, cfg->treeRanksPerNode > 0 ? cfg->treeRanksPerNode : n, cfg->treeIndex);
   c->devices.assign(n, 0);
@@ -1601,6 +1732,11 @@ NEXR_API nexrResult_t nexrPatAllGather(nexrRingComm_t c, const void* const* send
   return patCollective(c, false, sendbuffs, recvbuffs, sendcount, datatype, nexrSum);  // ncclAllGather: ncclSum
 }
 
+NEXR_API nexrResult_t nexrSendRecv(nexrRingComm_t c, const void* const* sendbuffs, const int* sendPeers,
+                                   void* const* recvbuffs, const int* recvPeers, size_t bytes) {
+  return sendRecv(c, sendbuffs, sendPeers, recvbuffs, recvPeers, bytes);
+}
+
 NEXR_API nexrResult_t nexrPatSchedule(int reduceScatter, int nRanks, int rank, size_t count, int datatype,
                                       size_t buffBytes, int64_t* ops, size_t capOps, size_t* nOps,
                                       int* parallelFactor) {
@@ -1639,6 +1775,7 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
   for (Conn* k : c->treeUp) freeConn(c, k);
   for (Conn* k : c->treeDown) freeConn(c, k);
   for (Conn* k : c->patConns) freeConn(c, k);
+  for (Conn* k : c->p2pConns) freeConn(c, k);
   for (auto* v : {&c->status, &c->status2})
     for (uint32_t* s : *v)
       if (s) {

@@ -19,7 +19,8 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrRingReduce", "nexrRingBroadcast", "nexrTreeAllReduce", "nexrTreeTopology",
                     "nexrRingCommDestroy", "nexrPeerRingCommCreate", "nexrPeerRingAllReduce",
                     "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
-                    "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule")
+                    "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
+                    "nexrSendRecv")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -74,6 +75,8 @@ def ring_lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.argtypes = [vp, vp, vp, sz, i32] + extra
             f.restype = ctypes.c_int
+        L.nexrSendRecv.argtypes = [vp, arr, ctypes.POINTER(i32), arr, ctypes.POINTER(i32), sz]
+        L.nexrSendRecv.restype = ctypes.c_int
         L.nexrPatSchedule.argtypes = [i32, i32, i32, sz, i32, sz, ctypes.POINTER(ctypes.c_int64), sz,
                                       ctypes.POINTER(sz), ctypes.POINTER(i32)]
         L.nexrPatSchedule.restype = ctypes.c_int
@@ -171,6 +174,14 @@ class RingComm:
         """ncclAllGather with NCCL_ALGO_PAT (SIMPLE)."""
         s, r = self._arrays(sendbuffs, recvbuffs)
         _check(ring_lib().nexrPatAllGather(self._h, s, r, int(sendcount), int(datatype)), "nexrPatAllGather")
+
+    def send_recv(self, sendbuffs, send_peers, recvbuffs, recv_peers, nbytes: int) -> None:
+        """ncclSend/ncclRecv of every rank in one group: rank r sends nbytes of sendbuffs[r] to
+        send_peers[r] and receives nbytes from recv_peers[r] into recvbuffs[r] (-1: none)."""
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        sp = (ctypes.c_int * self.n_ranks)(*[int(v) for v in send_peers])
+        rp = (ctypes.c_int * self.n_ranks)(*[int(v) for v in recv_peers])
+        _check(ring_lib().nexrSendRecv(self._h, s, sp, r, rp, int(nbytes)), "nexrSendRecv")
 
     def tree_topology(self, rank: int):
         """(up, [down...]) of `rank` in this communicator's tree (-1 = none)."""

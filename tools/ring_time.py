@@ -29,6 +29,8 @@ def run(n, mode_name, proto_name, coll, iters):
     # small integers: every sum order gives the same fp32 result, so numpy checks the schedule
     x = [rng.integers(-1000, 1000, count * n).astype(np.float32) for _ in range(n)]
     out_n = count * n if coll in ("allgather", "pat_ag") else count
+    if coll == "sendrecv":  # ring shift of the first 4 MiB of every rank's input
+        x = [v[:count].copy() for v in x]
     if mode == ring.DEVICE_MEMORY:
         send = [torch.from_numpy(v).cuda() for v in x]
         recv = [torch.zeros(out_n, dtype=torch.float32, device="cuda") for _ in range(n)]
@@ -45,7 +47,9 @@ def run(n, mode_name, proto_name, coll, iters):
                 "reducescatter": lambda: comm.reduce_scatter(sp, rp, count, F32, 0),
                 "allgather": lambda: comm.all_gather(sp, rp, count, F32),
                 "pat_rs": lambda: comm.pat_reduce_scatter(sp, rp, count, F32, 0),
-                "pat_ag": lambda: comm.pat_all_gather(sp, rp, count, F32)}[coll]
+                "pat_ag": lambda: comm.pat_all_gather(sp, rp, count, F32),
+                "sendrecv": lambda: comm.send_recv(sp, [(r + 1) % n for r in range(n)], rp,
+                                                   [(r - 1) % n for r in range(n)], count * 4)}[coll]
         call()
         t0 = time.perf_counter()
         for _ in range(iters):
@@ -56,6 +60,8 @@ def run(n, mode_name, proto_name, coll, iters):
         exp = [sum(v[:count] for v in x)] * n
     elif coll in ("reducescatter", "pat_rs"):
         exp = [sum(v[k * count:(k + 1) * count] for v in x) for k in range(n)]
+    elif coll == "sendrecv":
+        exp = [x[(r - 1) % n] for r in range(n)]
     else:
         exp = [np.concatenate([v[:count] for v in x])] * n
     assert all(np.array_equal(g, e) for g, e in zip(got, exp)), (n, mode_name, proto_name, coll)
@@ -64,11 +70,14 @@ def run(n, mode_name, proto_name, coll, iters):
 
 print(f"{'ranks':>5} {'mode':<10} {'proto':<6} {'collective':<14} {'ms/call':>9} {'algbw GB/s':>11}")
 for n in [int(v) for v in os.environ.get("RING_TIME_RANKS", "2,4").split(",")]:
+    modes = os.environ.get("RING_TIME_MODES", "cpu-oracle,host,device").split(",")
     for mode_name, protos in (("cpu-oracle", ("simple",)), ("host", ("simple",)),
                               ("device", ("simple", "ll", "ll128"))):
+        if mode_name not in modes:
+            continue
         for proto_name in protos:
             colls = ("allreduce", "tree", "reducescatter", "allgather")
-            for coll in colls + (("pat_rs", "pat_ag") if proto_name == "simple" else ()):
+            for coll in colls + (("pat_rs", "pat_ag", "sendrecv") if proto_name == "simple" else ()):
                 iters = 3 if mode_name == "cpu-oracle" else 10
                 dt = run(n, mode_name, proto_name, coll, iters)
                 print(f"{n:>5} {mode_name:<10} {proto_name:<6} {coll:<14} {dt * 1e3:9.3f} {count * 4 / dt / 1e9:11.2f}",
