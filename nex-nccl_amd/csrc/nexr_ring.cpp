@@ -236,11 +236,16 @@ struct Prims {
   // loadRecvConn / loadSendConn (prims_simple.h:512-513, :557-558): a SIMPLE Primitives starts each
   // connection at step roundUp(conn->step, SlicePerChunk*StepPerSlice), so a collective with 2-step
   // slices that follows one with 1-step slices (Broadcast, Reduce) never starts a slice in the last
-  // FIFO slot. Both endpoints of a connection hold the same step between collectives and round alike.
+  // FIFO slot. Both endpoints of a connection hold the same step between collectives and round alike,
+  // and the receiver publishes its rounded step as head ("return credits in case we rounded up",
+  // :514-517): the steps skipped by rounding were never sent, so the sender must not wait for them.
   void attach() {
     if (c->ll) return;
     const uint64_t cs = (uint64_t)(stepPerSlice * slicePerChunk);
-    for (int i = 0; i < nRecv; i++) recv[i]->recvStep = (recv[i]->recvStep + cs - 1) / cs * cs;
+    for (int i = 0; i < nRecv; i++) {
+      recv[i]->recvStep = (recv[i]->recvStep + cs - 1) / cs * cs;
+      recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
+    }
     for (int i = 0; i < nSend; i++) send[i]->sendStep = (send[i]->sendStep + cs - 1) / cs * cs;
   }
 

@@ -254,3 +254,20 @@ def test_tree_and_ring_share_one_comm(ring, oracle, fns):
             comm.all_reduce(_ptrs(x), _ptrs(out), x[0].size, mg.F32, 0)
             for r, e in enumerate(ring_allreduce_expected(x, mg.F32, 0, buff)):
                 assert out[r].tobytes() == e.tobytes()
+
+
+@pytest.mark.parametrize("steps", [9, 11, 13, 33, 35])
+def test_round_up_returns_credits(ring, oracle, fns, steps):
+    """Reduce + Broadcast (1-step slices) leave both ring links at an odd step; the next all-reduce
+    (2-step slices, 4-step chunks) rounds every link up, and the receiver must publish the rounded step
+    as its head ("return credits in case we rounded up", prims_simple.h:514-517) or the sender waits
+    forever for steps nobody sends (9, 13 and 33 steps hung before the fix)."""
+    n, count = 2, 1024 * steps  # 1 KiB... 4 KiB steps of uint32: `steps` steps per collective
+    x = [np.arange(count * n, dtype=np.uint32) * 7 + k for k in range(n)]
+    o = [np.zeros(count * n, np.uint32) for _ in range(n)]
+    with _comm(ring, fns, n, "simple", 8 * 4096) as comm:
+        comm.reduce(_ptrs(x), _ptrs(o), count, mg.U32, 0, 1)
+        comm.broadcast(_ptrs(x), _ptrs(o), count, mg.U32, 1)
+        comm.all_reduce(_ptrs(x), _ptrs(o), count, mg.U32, 0)
+    for r in range(n):
+        assert np.array_equal(o[r][:count], x[0][:count] + x[1][:count])
