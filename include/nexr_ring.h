@@ -174,6 +174,22 @@ typedef struct {
 NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* comm, const nexrPeerRingConfig* config);
 
 /* ncclAllReduce for this process's rank (sendbuff/recvbuff on config->device; in-place allowed). */
+/* PAT ReduceScatter / AllGather for this process's rank (arguments and restrictions as
+ * nexrPatReduceScatter / nexrPatAllGather). The first PAT call on a communicator connects the
+ * rank's r -/+ 2^d links through the shared segment (collective; up to 64 ranks). */
+NEXR_API nexrResult_t nexrPeerPatReduceScatter(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
+                                               size_t recvcount, int datatype, int op);
+NEXR_API nexrResult_t nexrPeerPatAllGather(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
+                                           size_t sendcount, int datatype);
+
+/* ncclSend / ncclRecv for this process's rank inside one group: send `bytes` of sendbuff to rank
+ * sendPeer and receive `bytes` from recvPeer into recvbuff (-1: none; sendPeer == recvPeer == own rank
+ * is a local copy). The send runs on a second thread beside the recv. The first call connects P2P
+ * links to every rank (collective: all ranks make their first call together; up to 64 ranks);
+ * afterwards every send must meet the matching recv on the peer in the same call. */
+NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t comm, const void* sendbuff, int sendPeer, void* recvbuff,
+                                       int recvPeer, size_t bytes);
+
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int op);
 

@@ -60,11 +60,13 @@ struct Conn {
 // the rendezvous, every connection's head/tail counters and a common abort word. Slot r belongs to
 // rank r: its FIFO's IPC handle and the counters of the connection INTO rank r.
 constexpr uint32_t kPeerMagic = 0x6e657872u;  // "nexr"
-struct PeerHeader {
+struct alignas(64) PeerHeader {
   std::atomic<uint32_t> initState;  // 0 fresh, 1 being configured, 2 configured
   std::atomic<uint32_t> joined;
   std::atomic<uint32_t> left;
   std::atomic<uint32_t> abort;
+  std::atomic<uint32_t> patJoined;  // ranks that published their PAT receive FIFOs
+  std::atomic<uint32_t> p2pJoined;  // ranks that published their P2P receive FIFOs
   uint32_t magic, nRanks, protocol, pad;
   uint64_t buffBytes;
 };
@@ -72,9 +74,23 @@ struct PeerSlot {
   hipIpcMemHandle_t fifoHandle;
   alignas(64) ConnState conn;
 };
-size_t peerShmBytes(int n) { return sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot); }
+// Links beyond the ring for PAT (r -> r +- 2^d) and P2P (any r -> q), one per ordered pair: the
+// receiver's FIFO handles and the link's counters. Only for communicators of up to kPeerLinkMaxRanks.
+constexpr int kPeerLinkMaxRanks = 64;
+struct PeerLink {
+  hipIpcMemHandle_t patFifo, p2pFifo;
+  alignas(64) ConnState pat;
+  alignas(64) ConnState p2p;
+};
+size_t peerShmBytes(int n) {
+  return sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot) +
+         (n <= kPeerLinkMaxRanks ? (size_t)n * n * sizeof(PeerLink) : 0);
+}
 PeerHeader* peerHeader(void* base) { return (PeerHeader*)base; }
 PeerSlot* peerSlot(void* base, int r) { return (PeerSlot*)((char*)base + sizeof(PeerHeader)) + r; }
+PeerLink* peerLink(void* base, int n, int from, int to) {
+  return (PeerLink*)((char*)base + sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot)) + (size_t)from * n + to;
+}
 
 int64_t divUp(int64_t a, int64_t b) { return (a + b - 1) / b; }
 int64_t alignUp(int64_t a, int64_t b) { return divUp(a, b) * b; }
@@ -1373,21 +1389,51 @@ nexrResult_t ensurePat(nexrRingComm* c) {
 }
 
 
+// One rank's PAT collective on the calling thread (thread ranks and process ranks alike).
+void runPatRank(nexrRingComm* c, Shared* sh, int rank, bool reduceScatter, const void* sendbuff, void* recvbuff,
+                size_t count, size_t esz, int datatype, const nexrDevRedOpFull& red) {
+  const int n = c->cfg.nRanks;
+  if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+  PatRank pr;
+  pr.p = makePrims(c, sh, rank, sendbuff, recvbuff, esz, datatype, red, kGeomPipe, c->streams[rank], c->status[rank]);
+  pr.reduceScatter = reduceScatter;
+  pr.stepElems = (int64_t)(c->stepBytes / esz);
+  for (int d = 0; d < kPatMaxDims && (1 << d) < n; d++) {
+    const int delta = 1 << d;
+    const int lo = (rank - delta + n) % n, hi = (rank + delta) % n;
+    // ReduceScatter receives from rank-2^d and sends to rank+2^d; AllGather the other way round.
+    const int recvPeer = reduceScatter ? lo : hi, sendPeer = reduceScatter ? hi : lo;
+    pr.recvDims[d].conn = patConn(c, recvPeer, rank);
+    pr.recvDims[d].step = pr.recvDims[d].conn->recvStep;
+    pr.sendDims[d].conn = patConn(c, rank, sendPeer);
+    pr.sendDims[d].step = pr.sendDims[d].conn->sendStep;
+  }
+  pr.run((int64_t)count, n);
+}
+
+// Argument checks shared by the thread-rank and process-rank PAT entry points.
+nexrResult_t patPrepare(nexrRingComm* c, bool reduceScatter, int datatype, int op, size_t count, size_t* esz,
+                        nexrDevRedOpFull* red) {
+  nexrResult_t r = prepare(c, datatype, op, esz, red);
+  if (r != nexrSuccess) return r;
+  // PAT runs SIMPLE only (tuning.cc:264) and never for ReduceScatter with a pre/post-op scaling
+  // (ncclAvg / user PreMulSum, enqueue.cc:1779-1780).
+  if (c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
+  if (reduceScatter && (red->op == nexrDevPreMulSum || red->op == nexrDevSumPostDiv)) return nexrInvalidArgument;
+  if (count > (size_t)INT32_MAX) return nexrInvalidArgument;  // ncclPatStep offsets are int
+  return nexrSuccess;
+}
+
 nexrResult_t patCollective(nexrRingComm* c, bool reduceScatter, const void* const* sendbuffs, void* const* recvbuffs,
                            size_t count, int datatype, int op) {
   if (!c || c->peer) return nexrInvalidArgument;
   size_t esz;
   nexrDevRedOpFull red;
-  nexrResult_t r = prepare(c, datatype, op, &esz, &red);
+  nexrResult_t r = patPrepare(c, reduceScatter, datatype, op, count, &esz, &red);
   if (r != nexrSuccess) return r;
-  // PAT runs SIMPLE only (tuning.cc:264) and never for ReduceScatter with a pre/post-op scaling
-  // (ncclAvg / user PreMulSum, enqueue.cc:1779-1780).
-  if (c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
-  if (reduceScatter && (red.op == nexrDevPreMulSum || red.op == nexrDevSumPostDiv)) return nexrInvalidArgument;
   const int n = c->cfg.nRanks;
   if (!sendbuffs || !recvbuffs) return nexrInvalidArgument;
   if (count == 0) return nexrSuccess;
-  if (count > (size_t)INT32_MAX) return nexrInvalidArgument;  // ncclPatStep offsets are int
   for (int i = 0; i < n; i++)
     if (!sendbuffs[i] || !recvbuffs[i]) return nexrInvalidArgument;
   if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
@@ -1398,27 +1444,10 @@ nexrResult_t patCollective(nexrRingComm* c, bool reduceScatter, const void* cons
   }
   Shared sh;
   std::vector<std::function<void()>> jobs;
-  for (int rank = 0; rank < n; rank++) {
+  for (int rank = 0; rank < n; rank++)
     jobs.emplace_back([&, rank] {
-      if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-      PatRank pr;
-      pr.p = makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, kGeomPipe, c->streams[rank],
-                       c->status[rank]);
-      pr.reduceScatter = reduceScatter;
-      pr.stepElems = (int64_t)(c->stepBytes / esz);
-      for (int d = 0; d < kPatMaxDims && (1 << d) < n; d++) {
-        const int delta = 1 << d;
-        const int lo = (rank - delta + n) % n, hi = (rank + delta) % n;
-        // ReduceScatter receives from rank-2^d and sends to rank+2^d; AllGather the other way round.
-        const int recvPeer = reduceScatter ? lo : hi, sendPeer = reduceScatter ? hi : lo;
-        pr.recvDims[d].conn = patConn(c, recvPeer, rank);
-        pr.recvDims[d].step = pr.recvDims[d].conn->recvStep;
-        pr.sendDims[d].conn = patConn(c, rank, sendPeer);
-        pr.sendDims[d].step = pr.sendDims[d].conn->sendStep;
-      }
-      pr.run((int64_t)count, n);
+      runPatRank(c, &sh, rank, reduceScatter, sendbuffs[rank], recvbuffs[rank], count, esz, datatype, red);
     });
-  }
   return runThreads(c, sh, jobs);
 }
 
@@ -1459,6 +1488,35 @@ nexrResult_t ensureP2p(nexrRingComm* c, const int* sendPeers) {
   return nexrSuccess;
 }
 
+// The halves of one rank's P2P work (sendrecv.h:174-194), each on the calling thread.
+void runSelfCopy(nexrRingComm* c, Shared* sh, int rank, const void* src, void* dst, size_t bytes) {
+  if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
+  nexrResult_t r = c->cfg.fn(1, &src, 1, &dst, bytes, nexrInt8, nexrDevSum, 0, 0, nullptr, 0,
+                             (nexrStream_t)c->streams[rank]);
+  if (r == nexrSuccess && c->streams[rank] && c->cfg.memMode == nexrRingDeviceMemory &&
+      hipStreamSynchronize(c->streams[rank]) != hipSuccess)
+    r = nexrUnhandledCudaError;
+  if (r != nexrSuccess) sh->fail(r);
+}
+
+void runP2pHalf(nexrRingComm* c, Shared* sh, int rank, bool send, int peer, const void* sendbuff, void* recvbuff,
+                size_t bytes) {
+  hipStream_t s = send ? c->streams[rank] : c->streams2[rank];
+  if (s) (void)hipSetDevice(c->devices[rank]);
+  const nexrDevRedOpFull copy = {nexrDevSum, 0, 0, 0};
+  Prims p = makePrims(c, sh, rank, sendbuff, recvbuff, 1, nexrInt8, copy, kGeomPipe, s, nullptr);
+  p.stepSize = (int64_t)c->p2pChunkBytes;  // Primitives' P2P stepSize argument (sendrecv.h:27-29)
+  if (send) p.send[p.nSend++] = p2pConn(c, rank, peer);
+  else p.recv[p.nRecv++] = p2pConn(c, peer, rank);
+  p.attach();
+  const int64_t chunk = (int64_t)u32fp8RoundTrip((uint32_t)c->p2pChunkBytes);
+  for (int64_t cursor = 0; cursor < (int64_t)bytes;) {  // runSend / runRecv (:15-62)
+    const int64_t m = std::min<int64_t>(chunk, (int64_t)bytes - cursor);
+    if (!(send ? p.sendInput(cursor, m) : p.recvOutput(cursor, m))) return;
+    cursor += m;
+  }
+}
+
 nexrResult_t sendRecv(nexrRingComm* c, const void* const* sendbuffs, const int* sendPeers, void* const* recvbuffs,
                       const int* recvPeers, size_t bytes) {
   if (!c || c->peer || !sendbuffs || !sendPeers || !recvbuffs || !recvPeers) return nexrInvalidArgument;
@@ -1479,57 +1537,19 @@ nexrResult_t sendRecv(nexrRingComm* c, const void* const* sendbuffs, const int* 
     c->broken = true;
     return res;
   }
-  const int64_t chunk = (int64_t)u32fp8RoundTrip((uint32_t)c->p2pChunkBytes);
-  const nexrDevRedOpFull copy = {nexrDevSum, 0, 0, 0};
   Shared sh;
   std::vector<std::function<void()>> jobs;
   for (int rank = 0; rank < n; rank++) {
     const int to = sendPeers[rank], from = recvPeers[rank];
     if (to == rank) {  // isCopy: one reduceCopy from the send buffer to the recv buffer
-      jobs.emplace_back([&, rank] {
-        if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-        const void* src = sendbuffs[rank];
-        void* dst = recvbuffs[rank];
-        nexrResult_t r = c->cfg.fn(1, &src, 1, &dst, bytes, nexrInt8, nexrDevSum, 0, 0, nullptr, 0,
-                                   (nexrStream_t)c->streams[rank]);
-        if (r == nexrSuccess && c->streams[rank] && c->cfg.memMode == nexrRingDeviceMemory &&
-            hipStreamSynchronize(c->streams[rank]) != hipSuccess)
-          r = nexrUnhandledCudaError;
-        if (r != nexrSuccess) sh.fail(r);
-      });
+      jobs.emplace_back([&, rank] { runSelfCopy(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], bytes); });
       continue;
     }
-    auto make = [&, rank](hipStream_t s) {
-      Prims p = makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], 1, nexrInt8, copy, kGeomPipe, s, nullptr);
-      p.stepSize = (int64_t)c->p2pChunkBytes;  // Primitives' P2P stepSize argument (sendrecv.h:27-29)
-      return p;
-    };
-    if (to >= 0) {
-      jobs.emplace_back([&, rank, to, make] {  // runSend
-        if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-        Prims p = make(c->streams[rank]);
-        p.send[p.nSend++] = p2pConn(c, rank, to);
-        p.attach();
-        for (int64_t cursor = 0; cursor < (int64_t)bytes;) {
-          const int64_t m = std::min<int64_t>(chunk, (int64_t)bytes - cursor);
-          if (!p.sendInput(cursor, m)) return;
-          cursor += m;
-        }
-      });
-    }
-    if (from >= 0) {
-      jobs.emplace_back([&, rank, from, make] {  // runRecv
-        if (c->streams2[rank]) (void)hipSetDevice(c->devices[rank]);
-        Prims p = make(c->streams2[rank]);
-        p.recv[p.nRecv++] = p2pConn(c, from, rank);
-        p.attach();
-        for (int64_t cursor = 0; cursor < (int64_t)bytes;) {
-          const int64_t m = std::min<int64_t>(chunk, (int64_t)bytes - cursor);
-          if (!p.recvOutput(cursor, m)) return;
-          cursor += m;
-        }
-      });
-    }
+    if (to >= 0)
+      jobs.emplace_back([&, rank, to] { runP2pHalf(c, &sh, rank, true, to, sendbuffs[rank], recvbuffs[rank], bytes); });
+    if (from >= 0)
+      jobs.emplace_back(
+          [&, rank, from] { runP2pHalf(c, &sh, rank, false, from, sendbuffs[rank], recvbuffs[rank], bytes); });
   }
   return runThreads(c, sh, jobs);
 }
@@ -1775,6 +1795,15 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
       c->conns[r]->st = &c->conns[r]->own;  // counters lived in the unmapped segment
       if ((int)r != c->self) c->conns[r]->fifo = nullptr;  // only this rank's FIFO is owned here
     }
+    for (auto* v : {&c->patConns, &c->p2pConns})
+      for (Conn* k : *v) {
+        if (!k) continue;
+        k->st = &k->own;
+        if (!k->ownsFifo && k->fifo) {
+          (void)hipIpcCloseMemHandle(k->fifo);
+          k->fifo = nullptr;
+        }
+      }
   }
   for (Conn* k : c->conns) freeConn(c, k);
   for (Conn* k : c->treeUp) freeConn(c, k);
@@ -1832,6 +1861,7 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   c->cfg.llFn = defaultLLFn;
   c->cfg.ll128Fn = defaultLL128Fn;
   c->stepBytes = c->cfg.buffBytes / kSteps;
+  c->p2pChunkBytes = std::min<size_t>(128 << 10, c->stepBytes);  // as nexrRingCommCreate
   c->peer = true;
   c->needHip = true;
   const int n = cfg->nRanks, me = cfg->rank, next = (me + 1) % n;
@@ -1917,6 +1947,149 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   }
   *out = c;
   return nexrSuccess;
+}
+
+}  // extern "C"
+
+namespace {
+
+bool isPatPair(int n, int from, int to) {
+  for (int d = 0; (1 << d) < n; d++)
+    if (to == (from + (1 << d)) % n || to == (from - (1 << d) + n) % n) return true;
+  return false;
+}
+
+// Process ranks: the first PAT (p2p = false) or Send/Recv (p2p = true) call on a communicator
+// connects this rank's extra links. Every rank allocates the FIFOs it receives into, publishes
+// their IPC handles in the shared segment, and, once all ranks have, maps the FIFOs it sends into.
+// Collective: every rank makes its first call of each kind together.
+nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
+  std::vector<Conn*>& conns = p2p ? c->p2pConns : c->patConns;
+  if (!conns.empty()) return nexrSuccess;
+  const int n = c->cfg.nRanks, me = c->self;
+  if (n > kPeerLinkMaxRanks) return nexrInvalidUsage;
+  conns.assign((size_t)n * n, nullptr);
+  auto isLink = [&](int from, int to) {
+    return from != to && (p2p || (to != (from + 1) % n && isPatPair(n, from, to)));  // r -> r+1 is the ring's
+  };
+  const size_t bytes = p2p ? c->p2pChunkBytes * kSteps : c->cfg.buffBytes;
+  const char* unc = getenv("NEXR_PEER_FIFO_UNCACHED");
+  const bool uncached = !(unc && unc[0] == '0');
+  if (hipSetDevice(c->devices[me]) != hipSuccess) return nexrUnhandledCudaError;
+  for (int q = 0; q < n; q++) {
+    if (!isLink(q, me)) continue;
+    PeerLink* l = peerLink(c->shm, n, q, me);
+    Conn* k = conns[(size_t)q * n + me] = new Conn();
+    k->device = c->devices[me];
+    k->slotBytes = p2p ? c->p2pChunkBytes : 0;
+    k->st = p2p ? &l->p2p : &l->pat;
+    if ((uncached ? hipExtMallocWithFlags((void**)&k->fifo, bytes, hipDeviceMallocUncached)
+                  : hipMalloc((void**)&k->fifo, bytes)) != hipSuccess ||
+        hipIpcGetMemHandle(p2p ? &l->p2pFifo : &l->patFifo, k->fifo) != hipSuccess)
+      return nexrUnhandledCudaError;
+  }
+  PeerHeader* h = peerHeader(c->shm);
+  std::atomic<uint32_t>& joined = p2p ? h->p2pJoined : h->patJoined;
+  joined.fetch_add(1, std::memory_order_acq_rel);  // publishes the handles
+  const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (joined.load(std::memory_order_acquire) < (uint32_t)n) {
+    if (h->abort.load(std::memory_order_acquire)) return nexrRemoteError;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return nexrRemoteError;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  for (int q = 0; q < n; q++) {
+    if (!isLink(me, q)) continue;
+    PeerLink* l = peerLink(c->shm, n, me, q);
+    Conn* k = conns[(size_t)me * n + q] = new Conn();
+    k->device = c->devices[me];
+    k->slotBytes = p2p ? c->p2pChunkBytes : 0;
+    k->st = p2p ? &l->p2p : &l->pat;
+    k->ownsFifo = false;
+    char* mapped = nullptr;
+    if (hipIpcOpenMemHandle((void**)&mapped, p2p ? l->p2pFifo : l->patFifo, hipIpcMemLazyEnablePeerAccess) !=
+        hipSuccess)
+      return nexrUnhandledCudaError;
+    k->fifo = mapped;
+  }
+  return nexrSuccess;
+}
+
+nexrResult_t peerFinish(nexrRingComm* c, Shared& sh) {
+  if (sh.firstError.load() != 0) {
+    c->broken = true;
+    return (nexrResult_t)sh.firstError.load();
+  }
+  return nexrSuccess;
+}
+
+nexrResult_t peerPat(nexrRingComm* c, bool reduceScatter, const void* sendbuff, void* recvbuff, size_t count,
+                     int datatype, int op) {
+  if (!c || !c->peer) return nexrInvalidArgument;
+  size_t esz;
+  nexrDevRedOpFull red;
+  nexrResult_t r = patPrepare(c, reduceScatter, datatype, op, count, &esz, &red);
+  if (r != nexrSuccess) return r;
+  if (count == 0) return nexrSuccess;
+  if (!sendbuff || !recvbuff) return nexrInvalidArgument;
+  const int me = c->self;
+  (void)hipSetDevice(c->devices[me]);
+  if (c->cfg.nRanks == 1) return oneRank(c, me, sendbuff, recvbuff, count, datatype, red, esz);
+  r = ensurePeerLinks(c, false);
+  if (r != nexrSuccess) {
+    c->broken = true;
+    if (c->shm) peerHeader(c->shm)->abort.store(1);
+    return r;
+  }
+  Shared sh;
+  sh.remoteAbort = &peerHeader(c->shm)->abort;
+  runPatRank(c, &sh, me, reduceScatter, sendbuff, recvbuff, count, esz, datatype, red);
+  return peerFinish(c, sh);
+}
+
+}  // namespace
+
+extern "C" {
+
+NEXR_API nexrResult_t nexrPeerPatReduceScatter(nexrRingComm_t c, const void* sendbuff, void* recvbuff,
+                                               size_t recvcount, int datatype, int op) {
+  return peerPat(c, true, sendbuff, recvbuff, recvcount, datatype, op);
+}
+
+NEXR_API nexrResult_t nexrPeerPatAllGather(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t sendcount,
+                                           int datatype) {
+  return peerPat(c, false, sendbuff, recvbuff, sendcount, datatype, nexrSum);
+}
+
+NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t c, const void* sendbuff, int sendPeer, void* recvbuff,
+                                       int recvPeer, size_t bytes) {
+  if (!c || !c->peer) return nexrInvalidArgument;
+  if (c->broken) return nexrInvalidUsage;
+  if (c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
+  const int n = c->cfg.nRanks, me = c->self;
+  if (sendPeer < -1 || sendPeer >= n || recvPeer < -1 || recvPeer >= n) return nexrInvalidArgument;
+  if ((sendPeer == me) != (recvPeer == me)) return nexrInvalidArgument;  // a self-send is its own recv
+  if (bytes > 0 && ((sendPeer >= 0 && !sendbuff) || (recvPeer >= 0 && !recvbuff))) return nexrInvalidArgument;
+  (void)hipSetDevice(c->devices[me]);
+  nexrResult_t r = n > 1 ? ensureSecondStreams(c) : nexrSuccess;
+  if (r == nexrSuccess && n > 1) r = ensurePeerLinks(c, true);
+  if (r != nexrSuccess) {
+    c->broken = true;
+    if (c->shm) peerHeader(c->shm)->abort.store(1);
+    return r;
+  }
+  if (bytes == 0) return nexrSuccess;
+  Shared sh;
+  sh.remoteAbort = &peerHeader(c->shm)->abort;
+  if (sendPeer == me) {
+    runSelfCopy(c, &sh, me, sendbuff, recvbuff, bytes);
+    return peerFinish(c, sh);
+  }
+  std::thread sender;
+  if (sendPeer >= 0) sender = std::thread([&] { runP2pHalf(c, &sh, me, true, sendPeer, sendbuff, recvbuff, bytes); });
+  if (recvPeer >= 0) runP2pHalf(c, &sh, me, false, recvPeer, sendbuff, recvbuff, bytes);
+  if (sender.joinable()) sender.join();
+  return peerFinish(c, sh);
 }
 
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,

@@ -20,7 +20,7 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrRingCommDestroy", "nexrPeerRingCommCreate", "nexrPeerRingAllReduce",
                     "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
                     "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
-                    "nexrSendRecv")
+                    "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -70,7 +70,10 @@ def ring_lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.argtypes = [vp, arr, arr, sz, i32] + extra
             f.restype = ctypes.c_int
+        L.nexrPeerSendRecv.argtypes = [vp, vp, i32, vp, i32, sz]
+        L.nexrPeerSendRecv.restype = ctypes.c_int
         for name, extra in (("nexrPeerRingReduceScatter", [i32]), ("nexrPeerRingAllGather", []),
+                            ("nexrPeerPatReduceScatter", [i32]), ("nexrPeerPatAllGather", []),
                             ("nexrPeerRingReduce", [i32, i32]), ("nexrPeerRingBroadcast", [i32])):
             f = getattr(L, name)
             f.argtypes = [vp, vp, vp, sz, i32] + extra
@@ -238,6 +241,18 @@ class PeerRingComm:
     def reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int, root: int) -> None:
         _check(ring_lib().nexrPeerRingReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
                                              int(datatype), int(op), int(root)), "nexrPeerRingReduce")
+
+    def pat_reduce_scatter(self, sendbuff: int, recvbuff: int, recvcount: int, datatype: int, op: int) -> None:
+        _check(ring_lib().nexrPeerPatReduceScatter(self._h, int(sendbuff) or None, int(recvbuff) or None,
+                                                   int(recvcount), int(datatype), int(op)), "nexrPeerPatReduceScatter")
+
+    def pat_all_gather(self, sendbuff: int, recvbuff: int, sendcount: int, datatype: int) -> None:
+        _check(ring_lib().nexrPeerPatAllGather(self._h, int(sendbuff) or None, int(recvbuff) or None, int(sendcount),
+                                               int(datatype)), "nexrPeerPatAllGather")
+
+    def send_recv(self, sendbuff: int, send_peer: int, recvbuff: int, recv_peer: int, nbytes: int) -> None:
+        _check(ring_lib().nexrPeerSendRecv(self._h, int(sendbuff) or None, int(send_peer), int(recvbuff) or None,
+                                           int(recv_peer), int(nbytes)), "nexrPeerSendRecv")
 
     def broadcast(self, sendbuff: int, recvbuff: int, count: int, datatype: int, root: int) -> None:
         _check(ring_lib().nexrPeerRingBroadcast(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),

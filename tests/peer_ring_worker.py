@@ -24,14 +24,15 @@ def main() -> int:
     for name in ("rank", "n", "dt", "op", "count", "seed", "proto", "buff", "calls"):
         ap.add_argument(f"--{name}", type=int, required=True)
     ap.add_argument("--coll", default="allreduce",
-                    choices=["allreduce", "reducescatter", "allgather", "reduce", "broadcast"])
+                    choices=["allreduce", "reducescatter", "allgather", "reduce", "broadcast", "pat_rs", "pat_ag",
+                             "sendrecv"])
     ap.add_argument("--root", type=int, default=0)
     ap.add_argument("--shm", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     ring = importlib.import_module("nex-nccl_amd.ring")
-    n_in = a.count * a.n if a.coll == "reducescatter" else a.count
-    n_out = a.count * a.n if a.coll == "allgather" else a.count
+    n_in = a.count * a.n if a.coll in ("reducescatter", "pat_rs") else a.count
+    n_out = a.count * a.n if a.coll in ("allgather", "pat_ag") else a.count
     inputs = mg.gen_inputs(a.dt, a.n, n_in, a.seed, special=True)
     dev = torch.device("cuda:0")
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
@@ -43,6 +44,14 @@ def main() -> int:
             for call in range(a.calls):
                 if a.coll == "reducescatter":
                     comm.reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+                elif a.coll == "pat_rs":
+                    comm.pat_reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+                elif a.coll == "pat_ag":
+                    comm.pat_all_gather(send.data_ptr(), recv.data_ptr(), a.count, a.dt)
+                elif a.coll == "sendrecv":  # call c: a ring shift by c+1 (a self-copy when it wraps)
+                    k = (call + 1) % a.n
+                    comm.send_recv(send.data_ptr(), (a.rank + k) % a.n, recv.data_ptr(), (a.rank - k) % a.n,
+                                   a.count * send.element_size())
                 elif a.coll == "allgather":
                     comm.all_gather(send.data_ptr(), recv.data_ptr(), a.count, a.dt)
                 elif a.coll == "reduce":

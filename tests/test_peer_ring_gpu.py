@@ -109,3 +109,41 @@ def test_peer_ring_other_collectives(oracle, tmp_path, coll, n, dt, op, proto, r
     for r in (range(n) if coll != "reduce" else [root]):
         for c in range(2):  # a second call on the same communicator: step counters carried over
             assert mg.canon_bytes(dt, outs[r][c]) == mg.canon_bytes(dt, exp[r]), f"rank {r}, call {c}"
+
+
+@pytest.mark.parametrize("n,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 0), (4, mg.I32, 2), (5, mg.F16, 1)])
+def test_peer_pat_reduce_scatter_processes(oracle, tmp_path, n, dt, op):
+    """PAT ReduceScatter with one process per rank: the r -/+ 2^d links are IPC-mapped FIFOs."""
+    from oracle import pat
+    count, buff = 30_001, 1 << 16
+    outs = _run_ring(tmp_path, n, dt, op, count, 0, buff, calls=2, coll="pat_rs")
+    inputs = mg.gen_inputs(dt, n, count * n, 7, special=True)
+    dev_op, arg = oracle.host_to_dev_red_op(op, dt, n)
+    exp = pat.reduce_scatter_expected(inputs, dt, dev_op, arg, buff // 8)
+    for r in range(n):
+        for c in range(2):
+            assert mg.canon_bytes(dt, outs[r][c]) == mg.canon_bytes(dt, exp[r]), f"rank {r}, call {c}"
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 6])
+def test_peer_pat_all_gather_processes(tmp_path, n):
+    count = 20_011
+    outs = _run_ring(tmp_path, n, mg.F16, 0, count, 0, 1 << 15, calls=2, coll="pat_ag")
+    inputs = mg.gen_inputs(mg.F16, n, count, 7, special=True)
+    exp = np.concatenate(inputs).tobytes()
+    for r in range(n):
+        for c in range(2):
+            assert outs[r][c].tobytes() == exp, f"rank {r}, call {c}"
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_peer_send_recv_processes(tmp_path, n):
+    """Send/Recv with one process per rank: call c shifts by c+1 (a local copy when it wraps to 0)."""
+    count = 300_007
+    calls = n + 1
+    outs = _run_ring(tmp_path, n, mg.I32, 0, count, 0, 1 << 16, calls=calls, coll="sendrecv")
+    inputs = mg.gen_inputs(mg.I32, n, count, 7, special=True)
+    for r in range(n):
+        for c in range(calls):
+            k = (c + 1) % n
+            assert outs[r][c].tobytes() == inputs[(r - k) % n].tobytes(), f"rank {r}, call {c}"
