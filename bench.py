@@ -60,12 +60,20 @@ def algorithmic_bytes(cfg) -> int:
 
 
 # ---- distributed plumbing (harness only: no data-path collective) -----------------------------
+def local_device_index() -> int:
+    """This rank's GPU: LOCAL_RANK, folded onto the visible devices (a launcher that gives every rank
+    one visible GPU, or a rehearsal with more ranks than GPUs, still lands on a valid device)."""
+    import torch
+    return int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+
+
 class Dist:
     def __init__(self, backend: str | None):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.local_rank = local_device_index() if backend == "nccl" else int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
+        self.backend = backend
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -84,7 +92,7 @@ class Dist:
         if not self.pg:
             return value
         import torch
-        t = torch.tensor([value], dtype=torch.float64, device=device)
+        t = torch.tensor([value], dtype=torch.float64, device=device if self.backend == "nccl" else None)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
@@ -176,10 +184,12 @@ def main(argv=None):
     import torch
 
     cfg = CONFIGS[args.config]
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = local_device_index()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    dist = Dist("nccl")
+    # NEXR_BENCH_BACKEND=gloo: rehearse the N > 1 harness where RCCL cannot run (several ranks on one
+    # GPU); the barrier and max-over-ranks timer are the only collectives either way.
+    dist = Dist(os.environ.get("NEXR_BENCH_BACKEND", "nccl"))
     if dist.world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={dist.world}")
     pkg = importlib.import_module("nex-nccl_amd")
