@@ -127,8 +127,9 @@ NEXR_API nexrResult_t nexrPatAllGather(nexrRingComm_t comm, const void* const* s
  * send must meet the matching recv (recvPeers[sendPeers[r]] == r), else nexrInvalidArgument. A
  * rank's send and recv run concurrently on its two streams over connection-index-1 FIFOs with
  * 8 steps of the P2P chunk size (128 KiB, at most buffBytes/8); a send to self is one copy.
- * SIMPLE protocol only: the reference's LL path for messages <= 16 KiB (enqueue.cc:786-839) is not
- * restated (nexrInvalidUsage on an LL/LL128 communicator). */
+ * Messages of at most 16 KiB move as LL lines (enqueue.cc:786-839) when the LL step can reach them
+ * (device memory, or a caller-supplied llFn), else as SIMPLE chunks. The communicator's own protocol
+ * must be SIMPLE (nexrInvalidUsage otherwise). */
 NEXR_API nexrResult_t nexrSendRecv(nexrRingComm_t comm, const void* const* sendbuffs, const int* sendPeers,
                                    void* const* recvbuffs, const int* recvPeers, size_t bytes);
 

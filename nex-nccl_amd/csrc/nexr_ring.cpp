@@ -78,9 +78,10 @@ struct PeerSlot {
 // receiver's FIFO handles and the link's counters. Only for communicators of up to kPeerLinkMaxRanks.
 constexpr int kPeerLinkMaxRanks = 64;
 struct PeerLink {
-  hipIpcMemHandle_t patFifo, p2pFifo;
+  hipIpcMemHandle_t patFifo, p2pFifo, p2pLLFifo;
   alignas(64) ConnState pat;
   alignas(64) ConnState p2p;
+  alignas(64) ConnState p2pLL;
 };
 size_t peerShmBytes(int n) {
   return sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot) +
@@ -186,6 +187,7 @@ struct nexrRingComm {
   std::vector<Conn*> treeDown;  // treeDown[r]: parent(r) -> r (broadcast)
   std::vector<Conn*> patConns;  // PAT: patConns[from*nRanks+to] for to = from +- 2^d (ring link excluded)
   std::vector<Conn*> p2pConns;  // ncclSend/ncclRecv: p2pConns[from*nRanks+to] (connIndex 1), made on first use
+  std::vector<Conn*> p2pLLConns;  // the same links' LL buffers, for messages <= 16 KiB
   size_t p2pChunkBytes = 0;     // comm->p2pChunkSize
   std::vector<int> devices;
   std::vector<hipStream_t> streams, streams2;  // streams2: the tree's broadcast-half threads
@@ -245,6 +247,7 @@ struct Prims {
   uint32_t* status;
   hipStream_t stream;
   bool device;
+  int proto = nexrRingProtoSimple;  // the communicator's, or LL for a small P2P message (sendrecv.h)
 
   char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
   size_t slot(const Conn* q) const { return q->slotBytes ? q->slotBytes : c->stepBytes; }
@@ -256,7 +259,7 @@ struct Prims {
   // and the receiver publishes its rounded step as head ("return credits in case we rounded up",
   // :514-517): the steps skipped by rounding were never sent, so the sender must not wait for them.
   void attach() {
-    if (c->ll) return;
+    if (proto != nexrRingProtoSimple) return;
     const uint64_t cs = (uint64_t)(stepPerSlice * slicePerChunk);
     for (int i = 0; i < nRecv; i++) {
       recv[i]->recvStep = (recv[i]->recvStep + cs - 1) / cs * cs;
@@ -365,12 +368,12 @@ struct Prims {
       uint32_t rf32[kMaxArity], sf32[kMaxArity];
       uint64_t rf64[kMaxArity], sf64[kMaxArity];
       for (int i = 0; i < nr; i++) {
-        recvLines[i] = recv[i]->fifo + (recv[i]->recvStep % kSteps) * c->stepBytes;
+        recvLines[i] = recv[i]->fifo + (recv[i]->recvStep % kSteps) * slot(recv[i]);
         rf64[i] = recv[i]->recvStep + 1;
         rf32[i] = (uint32_t)rf64[i];
       }
       for (int i = 0; i < ns; i++) {
-        sendLines[i] = send[i]->fifo + (send[i]->sendStep % kSteps) * c->stepBytes;
+        sendLines[i] = send[i]->fifo + (send[i]->sendStep % kSteps) * slot(send[i]);
         sf64[i] = send[i]->sendStep + 1;
         sf32[i] = (uint32_t)sf64[i];
       }
@@ -380,7 +383,7 @@ struct Prims {
       if (status) *status = 0;
       const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
       nexrResult_t r;
-      if (c->proto == nexrRingProtoLL128)
+      if (proto == nexrRingProtoLL128)
         r = ll128Fn(src, srcIsInput, nr, recvLines, rf64, dst, ns, sendLines, sf64, (size_t)nelem, datatype, devOp,
                     redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
       else
@@ -404,7 +407,7 @@ struct Prims {
     return true;
   }
   bool op(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t n, bool postOp) {
-    return c->ll ? genericOpLL(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp)
+    return proto != nexrRingProtoSimple ? genericOpLL(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp)
                  : genericOp(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp);
   }
   // The primitives the schedules use (prims_simple.h:897-976; the direct* forms reduce to these
@@ -612,6 +615,7 @@ Prims makePrims(nexrRingComm* c, Shared* sh, int rank, const void* sendbuff, voi
   p.status = status;
   p.stream = stream;
   p.device = c->cfg.memMode == nexrRingDeviceMemory;
+  p.proto = c->proto;
   return p;
 }
 
@@ -664,13 +668,14 @@ nexrResult_t runThreads(nexrRingComm* c, Shared& sh, const std::vector<std::func
   return nexrSuccess;
 }
 
-nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device) {
+nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes = 0) {
   k->device = device;
+  if (bytes == 0) bytes = c->cfg.buffBytes;
   if (c->cfg.memMode == nexrRingDeviceMemory) {
-    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, c->cfg.buffBytes) != hipSuccess)
+    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, bytes) != hipSuccess)
       return nexrUnhandledCudaError;
   } else {
-    k->fifo = (char*)aligned_alloc(4096, c->cfg.buffBytes);
+    k->fifo = (char*)aligned_alloc(4096, bytes);
     if (!k->fifo) return nexrSystemError;
   }
   return nexrSuccess;
@@ -1470,18 +1475,30 @@ uint32_t u32fp8RoundTrip(uint32_t x) {
   return m << expo;
 }
 
-Conn* p2pConn(nexrRingComm* c, int from, int to) { return c->p2pConns[(size_t)from * c->cfg.nRanks + to]; }
+Conn* p2pConn(nexrRingComm* c, int from, int to, bool ll) {
+  return (ll ? c->p2pLLConns : c->p2pConns)[(size_t)from * c->cfg.nRanks + to];
+}
 
-nexrResult_t ensureP2p(nexrRingComm* c, const int* sendPeers) {
+// P2P messages of at most this many bytes take the LL protocol (NCCL_P2P_LL_THRESHOLD x 1 channel,
+// enqueue.cc:786, :825-839), when an LL step implementation can reach the FIFO lines: device
+// memory, or a caller-supplied llFn. Self-sends never do (:805).
+constexpr size_t kP2pLLThreshold = 16384;
+bool p2pUsesLL(const nexrRingComm* c, size_t bytes) {
+  return bytes <= kP2pLLThreshold && (c->cfg.memMode == nexrRingDeviceMemory || c->cfg.llFn != defaultLLFn);
+}
+
+nexrResult_t ensureP2p(nexrRingComm* c, const int* sendPeers, bool ll) {
   const int n = c->cfg.nRanks;
-  if (c->p2pConns.empty()) c->p2pConns.assign((size_t)n * n, nullptr);
+  std::vector<Conn*>& conns = ll ? c->p2pLLConns : c->p2pConns;
+  if (conns.empty()) conns.assign((size_t)n * n, nullptr);
   for (int r = 0; r < n; r++) {
     const int q = sendPeers[r];
-    if (q < 0 || q == r || p2pConn(c, r, q)) continue;
+    if (q < 0 || q == r || p2pConn(c, r, q, ll)) continue;
     Conn* k = new Conn();
-    c->p2pConns[(size_t)r * n + q] = k;
-    k->slotBytes = c->p2pChunkBytes;
-    nexrResult_t res = allocFifo(c, k, c->devices[q]);
+    conns[(size_t)r * n + q] = k;
+    // SIMPLE: 8 steps of the P2P chunk; LL: the LL buffer's 8 steps of 64 KiB lines (init.cc:618)
+    k->slotBytes = ll ? kDefaultLLBuffBytes / kSteps : c->p2pChunkBytes;
+    nexrResult_t res = allocFifo(c, k, c->devices[q], ll ? kDefaultLLBuffBytes : 0);
     if (res == nexrSuccess && c->cfg.memMode == nexrRingDeviceMemory) res = enablePeer(c->devices[r], c->devices[q]);
     if (res != nexrSuccess) return res;
   }
@@ -1504,12 +1521,17 @@ void runP2pHalf(nexrRingComm* c, Shared* sh, int rank, bool send, int peer, cons
   hipStream_t s = send ? c->streams[rank] : c->streams2[rank];
   if (s) (void)hipSetDevice(c->devices[rank]);
   const nexrDevRedOpFull copy = {nexrDevSum, 0, 0, 0};
-  Prims p = makePrims(c, sh, rank, sendbuff, recvbuff, 1, nexrInt8, copy, kGeomPipe, s, nullptr);
+  const bool ll = p2pUsesLL(c, bytes);
+  Prims p = makePrims(c, sh, rank, sendbuff, recvbuff, 1, nexrInt8, copy, kGeomPipe, s,
+                      send ? c->status[rank] : c->status2[rank]);
+  p.proto = ll ? nexrRingProtoLL : nexrRingProtoSimple;
   p.stepSize = (int64_t)c->p2pChunkBytes;  // Primitives' P2P stepSize argument (sendrecv.h:27-29)
-  if (send) p.send[p.nSend++] = p2pConn(c, rank, peer);
-  else p.recv[p.nRecv++] = p2pConn(c, peer, rank);
+  if (send) p.send[p.nSend++] = p2pConn(c, rank, peer, ll);
+  else p.recv[p.nRecv++] = p2pConn(c, peer, rank, ll);
   p.attach();
-  const int64_t chunk = (int64_t)u32fp8RoundTrip((uint32_t)c->p2pChunkBytes);
+  // The chunk (enqueue.cc:840-856): SIMPLE moves p2pChunkSize per chunk, LL half an LL step of data;
+  // either way after the 8-bit u32fp8 round trip of the work descriptor.
+  const int64_t chunk = (int64_t)u32fp8RoundTrip((uint32_t)(ll ? kDefaultLLBuffBytes / kSteps / 2 : c->p2pChunkBytes));
   for (int64_t cursor = 0; cursor < (int64_t)bytes;) {  // runSend / runRecv (:15-62)
     const int64_t m = std::min<int64_t>(chunk, (int64_t)bytes - cursor);
     if (!(send ? p.sendInput(cursor, m) : p.recvOutput(cursor, m))) return;
@@ -1532,7 +1554,7 @@ nexrResult_t sendRecv(nexrRingComm* c, const void* const* sendbuffs, const int* 
   }
   if (bytes == 0) return nexrSuccess;
   nexrResult_t res = ensureSecondStreams(c);
-  if (res == nexrSuccess) res = ensureP2p(c, sendPeers);
+  if (res == nexrSuccess) res = ensureP2p(c, sendPeers, p2pUsesLL(c, bytes));
   if (res != nexrSuccess) {
     c->broken = true;
     return res;
@@ -1795,7 +1817,7 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
       c->conns[r]->st = &c->conns[r]->own;  // counters lived in the unmapped segment
       if ((int)r != c->self) c->conns[r]->fifo = nullptr;  // only this rank's FIFO is owned here
     }
-    for (auto* v : {&c->patConns, &c->p2pConns})
+    for (auto* v : {&c->patConns, &c->p2pConns, &c->p2pLLConns})
       for (Conn* k : *v) {
         if (!k) continue;
         k->st = &k->own;
@@ -1810,6 +1832,7 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
   for (Conn* k : c->treeDown) freeConn(c, k);
   for (Conn* k : c->patConns) freeConn(c, k);
   for (Conn* k : c->p2pConns) freeConn(c, k);
+  for (Conn* k : c->p2pLLConns) freeConn(c, k);
   for (auto* v : {&c->status, &c->status2})
     for (uint32_t* s : *v)
       if (s) {
@@ -1964,29 +1987,45 @@ bool isPatPair(int n, int from, int to) {
 // their IPC handles in the shared segment, and, once all ranks have, maps the FIFOs it sends into.
 // Collective: every rank makes its first call of each kind together.
 nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
-  std::vector<Conn*>& conns = p2p ? c->p2pConns : c->patConns;
-  if (!conns.empty()) return nexrSuccess;
+  std::vector<Conn*>& first = p2p ? c->p2pConns : c->patConns;
+  if (!first.empty()) return nexrSuccess;
   const int n = c->cfg.nRanks, me = c->self;
   if (n > kPeerLinkMaxRanks) return nexrInvalidUsage;
-  conns.assign((size_t)n * n, nullptr);
   auto isLink = [&](int from, int to) {
     return from != to && (p2p || (to != (from + 1) % n && isPatPair(n, from, to)));  // r -> r+1 is the ring's
   };
-  const size_t bytes = p2p ? c->p2pChunkBytes * kSteps : c->cfg.buffBytes;
+  // The link sets this kind connects: PAT's; or P2P's SIMPLE buffers and their LL buffers.
+  struct Set {
+    std::vector<Conn*>* conns;
+    size_t bytes, slot;
+    ConnState PeerLink::*state;
+    hipIpcMemHandle_t PeerLink::*handle;
+  };
+  std::vector<Set> sets;
+  if (p2p) {
+    sets.push_back({&c->p2pConns, c->p2pChunkBytes * kSteps, c->p2pChunkBytes, &PeerLink::p2p, &PeerLink::p2pFifo});
+    sets.push_back({&c->p2pLLConns, kDefaultLLBuffBytes, kDefaultLLBuffBytes / kSteps, &PeerLink::p2pLL,
+                    &PeerLink::p2pLLFifo});
+  } else {
+    sets.push_back({&c->patConns, c->cfg.buffBytes, 0, &PeerLink::pat, &PeerLink::patFifo});
+  }
   const char* unc = getenv("NEXR_PEER_FIFO_UNCACHED");
   const bool uncached = !(unc && unc[0] == '0');
   if (hipSetDevice(c->devices[me]) != hipSuccess) return nexrUnhandledCudaError;
-  for (int q = 0; q < n; q++) {
-    if (!isLink(q, me)) continue;
-    PeerLink* l = peerLink(c->shm, n, q, me);
-    Conn* k = conns[(size_t)q * n + me] = new Conn();
-    k->device = c->devices[me];
-    k->slotBytes = p2p ? c->p2pChunkBytes : 0;
-    k->st = p2p ? &l->p2p : &l->pat;
-    if ((uncached ? hipExtMallocWithFlags((void**)&k->fifo, bytes, hipDeviceMallocUncached)
-                  : hipMalloc((void**)&k->fifo, bytes)) != hipSuccess ||
-        hipIpcGetMemHandle(p2p ? &l->p2pFifo : &l->patFifo, k->fifo) != hipSuccess)
-      return nexrUnhandledCudaError;
+  for (Set& st : sets) {
+    st.conns->assign((size_t)n * n, nullptr);
+    for (int q = 0; q < n; q++) {
+      if (!isLink(q, me)) continue;
+      PeerLink* l = peerLink(c->shm, n, q, me);
+      Conn* k = (*st.conns)[(size_t)q * n + me] = new Conn();
+      k->device = c->devices[me];
+      k->slotBytes = st.slot;
+      k->st = &(l->*st.state);
+      if ((uncached ? hipExtMallocWithFlags((void**)&k->fifo, st.bytes, hipDeviceMallocUncached)
+                    : hipMalloc((void**)&k->fifo, st.bytes)) != hipSuccess ||
+          hipIpcGetMemHandle(&(l->*st.handle), k->fifo) != hipSuccess)
+        return nexrUnhandledCudaError;
+    }
   }
   PeerHeader* h = peerHeader(c->shm);
   std::atomic<uint32_t>& joined = p2p ? h->p2pJoined : h->patJoined;
@@ -1998,19 +2037,20 @@ nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return nexrRemoteError;
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
-  for (int q = 0; q < n; q++) {
-    if (!isLink(me, q)) continue;
-    PeerLink* l = peerLink(c->shm, n, me, q);
-    Conn* k = conns[(size_t)me * n + q] = new Conn();
-    k->device = c->devices[me];
-    k->slotBytes = p2p ? c->p2pChunkBytes : 0;
-    k->st = p2p ? &l->p2p : &l->pat;
-    k->ownsFifo = false;
-    char* mapped = nullptr;
-    if (hipIpcOpenMemHandle((void**)&mapped, p2p ? l->p2pFifo : l->patFifo, hipIpcMemLazyEnablePeerAccess) !=
-        hipSuccess)
-      return nexrUnhandledCudaError;
-    k->fifo = mapped;
+  for (Set& st : sets) {
+    for (int q = 0; q < n; q++) {
+      if (!isLink(me, q)) continue;
+      PeerLink* l = peerLink(c->shm, n, me, q);
+      Conn* k = (*st.conns)[(size_t)me * n + q] = new Conn();
+      k->device = c->devices[me];
+      k->slotBytes = st.slot;
+      k->st = &(l->*st.state);
+      k->ownsFifo = false;
+      char* mapped = nullptr;
+      if (hipIpcOpenMemHandle((void**)&mapped, l->*st.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+        return nexrUnhandledCudaError;
+      k->fifo = mapped;
+    }
   }
   return nexrSuccess;
 }

@@ -136,10 +136,10 @@ def test_peer_pat_all_gather_processes(tmp_path, n):
             assert outs[r][c].tobytes() == exp, f"rank {r}, call {c}"
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
-def test_peer_send_recv_processes(tmp_path, n):
-    """Send/Recv with one process per rank: call c shifts by c+1 (a local copy when it wraps to 0)."""
-    count = 300_007
+@pytest.mark.parametrize("n,count", [(2, 300_007), (3, 300_007), (4, 300_007), (3, 1_001)])
+def test_peer_send_recv_processes(tmp_path, n, count):
+    """Send/Recv with one process per rank: call c shifts by c+1 (a local copy when it wraps to 0);
+    4,004-byte messages take the LL links."""
     calls = n + 1
     outs = _run_ring(tmp_path, n, mg.I32, 0, count, 0, 1 << 16, calls=calls, coll="sendrecv")
     inputs = mg.gen_inputs(mg.I32, n, count, 7, special=True)

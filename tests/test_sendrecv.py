@@ -81,3 +81,42 @@ def test_send_recv_rejects_unmatched(ring, fn, nexr):
     with ring.RingComm(2, ring.HOST_MEMORY, 8 * 1024, fn, 20000, ring.PROTO_LL, fn, fn) as comm:
         with pytest.raises(nexr.NexrError):
             comm.send_recv(ptrs[:2], [1, 0], ptrs[:2], [1, 0], 64)
+
+
+_LL_ARGS = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+            ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+LL_CALLS = []
+
+
+@pytest.fixture(scope="module")
+def ll_fn(oracle):
+    """The oracle's LL step behind a counting trampoline (nexrReduceCopyLLFn signature)."""
+    target = oracle.lib().oracle_reduce_copy_ll_fn
+    target.argtypes, target.restype = _LL_ARGS, ctypes.c_int
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, *_LL_ARGS)
+
+    def tramp(*args):
+        LL_CALLS.append(args[9])  # nElts of the step
+        return target(*args)
+
+    cb = proto(tramp)
+    ll_fn.keep = cb  # keep the trampoline alive for the module
+    return ctypes.cast(cb, ctypes.c_void_p).value
+
+
+@pytest.mark.parametrize("nbytes", [1, 8, 15, 1000, 16_384, 16_385, 40_000])
+def test_small_messages_take_ll(ring, fn, ll_fn, nbytes):
+    """Messages up to 16 KiB travel as LL lines (NCCL_P2P_LL_THRESHOLD, enqueue.cc:786-839) when an LL
+    step implementation is available (here the oracle's); larger ones as SIMPLE chunks. Both kinds of
+    link persist on one communicator, with self-sends (plain copies) in between."""
+    n = 4
+    LL_CALLS.clear()
+    with ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, fn, 20000, ring.PROTO_SIMPLE, ll_fn) as comm:
+        for it, shift in enumerate((1, 3, 0, 2, 1)):
+            _run(ring, fn, n, [(r + shift) % n for r in range(n)], [(r - shift) % n for r in range(n)],
+                 nbytes if it % 2 == 0 else 20_000, comm=comm, seed=it)
+    # calls 0 and 4 move `nbytes` between distinct ranks (call 2 is a self-send): one LL step per
+    # send and per recv, each carrying the whole message
+    expect = 2 * 2 * n if nbytes <= 16_384 else 0
+    assert len(LL_CALLS) == expect and all(v == nbytes for v in LL_CALLS)

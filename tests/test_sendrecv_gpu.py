@@ -17,7 +17,9 @@ def ring(nexr):
 
 
 @pytest.mark.parametrize("n,shift,nbytes,buff", [(2, 1, 3_000_001, 0), (4, 1, 1 << 20, 1 << 16), (5, 2, 77_777, 1 << 15),
-                                                 (8, 3, 1 << 22, 0), (3, 0, 123_457, 0)])
+                                                 (8, 3, 1 << 22, 0), (3, 0, 123_457, 0),
+                                                 # <= 16 KiB: the LL protocol (nexrReduceCopyLL steps)
+                                                 (2, 1, 1, 0), (3, 1, 4_097, 0), (4, 3, 16_384, 1 << 16)])
 def test_send_recv_device(ring, n, shift, nbytes, buff):
     g = torch.Generator(device="cuda")
     g.manual_seed(n * 7 + shift)
