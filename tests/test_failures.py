@@ -1,0 +1,88 @@
+"""Failure paths of the emulated collectives (CPU): a reduce-copy step that fails, or one that stalls
+past the communicator's timeout, must end the collective on EVERY rank promptly with the reference's
+error convention (the failing step's ncclResult_t; ncclInternalError for a timed-out wait, as
+checkAbort gives up, primitives.h:142-156), and the communicator must refuse further work
+(nexrInvalidUsage) because its step counters are mid-protocol. Every reduceCopy is served by the
+oracle behind a Python trampoline that injects the failure."""
+import ctypes
+import importlib
+import threading
+import time
+
+import numpy as np
+import pytest
+
+U32 = 3
+
+
+@pytest.fixture(scope="module")
+def ring(nexr):
+    return importlib.import_module("nex-nccl_amd.ring")
+
+
+_ARGS = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+         ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+
+
+class Injector:
+    """A nexrReduceCopyFn that forwards to the oracle and misbehaves on call number `at`."""
+
+    def __init__(self, oracle, at, mode):
+        self.target = oracle.lib().oracle_reduce_copy_fn
+        self.target.argtypes, self.target.restype = _ARGS, ctypes.c_int
+        self.at, self.mode, self.calls = at, mode, 0
+        self.lock = threading.Lock()
+        self.cb = ctypes.CFUNCTYPE(ctypes.c_int, *_ARGS)(self._call)
+
+    def _call(self, *args):
+        with self.lock:
+            self.calls += 1
+            k = self.calls
+        if k == self.at:
+            if self.mode == "fail":
+                return 1  # ncclUnhandledCudaError
+            time.sleep(1.5)  # stall past the 300 ms wait bound of every other rank
+        return self.target(*args)
+
+    @property
+    def address(self):
+        return ctypes.cast(self.cb, ctypes.c_void_p).value
+
+
+def _run(comm, kind, n, count):
+    x = [np.arange(count * n, dtype=np.uint32) + r for r in range(n)]
+    o = [np.zeros(count * n, np.uint32) for _ in range(n)]
+    xp, op = [v.ctypes.data for v in x], [v.ctypes.data for v in o]
+    {"ring": lambda: comm.all_reduce(xp, op, count, U32, 0),
+     "tree": lambda: comm.tree_all_reduce(xp, op, count, U32, 0),
+     "pat_rs": lambda: comm.pat_reduce_scatter(xp, op, count, U32, 0),
+     "pat_ag": lambda: comm.pat_all_gather(xp, op, count, U32),
+     "sendrecv": lambda: comm.send_recv(xp, [(r + 1) % n for r in range(n)], op, [(r - 1) % n for r in range(n)],
+                                        count * 4)}[kind]()
+
+
+@pytest.mark.parametrize("kind", ["ring", "tree", "pat_rs", "pat_ag", "sendrecv"])
+@pytest.mark.parametrize("mode,code", [("fail", 1), ("stall", 3)])
+def test_step_failure_ends_every_rank(ring, oracle, nexr, kind, mode, code):
+    n, count = 4, 20_000
+    inj = Injector(oracle, at=5, mode=mode)
+    with ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, inj.address, 300, 0, None, None, 2) as comm:
+        t0 = time.perf_counter()
+        with pytest.raises(nexr.NexrError) as e:
+            _run(comm, kind, n, count)
+        assert e.value.code == code
+        assert time.perf_counter() - t0 < 10  # every rank gave up; nobody waited for a full timeout chain
+        with pytest.raises(nexr.NexrError) as e2:
+            _run(comm, kind, n, count)
+        assert e2.value.code == nexr.Result.InvalidUsage  # counters are mid-protocol: comm is broken
+
+
+def test_healthy_comm_after_a_broken_one(ring, oracle):
+    """A broken communicator does not affect a fresh one."""
+    good = Injector(oracle, at=-1, mode="fail")
+    n, count = 3, 5_000
+    with ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, good.address, 20000) as comm:
+        x = [np.arange(count, dtype=np.uint32) * (r + 1) for r in range(n)]
+        o = [np.zeros(count, np.uint32) for _ in range(n)]
+        comm.all_reduce([v.ctypes.data for v in x], [v.ctypes.data for v in o], count, U32, 0)
+        assert all(np.array_equal(v, np.arange(count, dtype=np.uint32) * 6) for v in o)
