@@ -350,27 +350,33 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
   // 80.7 GB/s vs 71.5 GB/s staged for the C2 mix: profiles/r01_h2d_probe.log).
   const void* zsrc[NEXR_MAX_SRCS];
   void* zdst[NEXR_MAX_DSTS];
+  bool psrc[NEXR_MAX_SRCS], pdst[NEXR_MAX_DSTS];  // pinned (device-mapped) buffers
   static const long zeroCopy = envLong("NEXR_HOST_ZERO_COPY", 1);
-  bool pinned = zeroCopy != 0;
-  for (int k = 0; pinned && k < nSrcs + nDsts; k++) {
+  int nPinned = 0;
+  for (int k = 0; k < nSrcs + nDsts; k++) {
     const void* hp = k < nSrcs ? srcs[k] : dsts[k - nSrcs];
     hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, hp) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
-      (void)hipGetLastError();  // pageable memory reports an error: not a failure of this call
-      pinned = false;
-      break;
+    bool pin = zeroCopy != 0 && hipPointerGetAttributes(&a, hp) == hipSuccess && a.type == hipMemoryTypeHost &&
+               a.devicePointer != nullptr;
+    if (!pin) (void)hipGetLastError();  // pageable memory reports an error: not a failure of this call
+    if (k < nSrcs) {
+      psrc[k] = pin;
+      zsrc[k] = pin ? a.devicePointer : nullptr;
+    } else {
+      pdst[k - nSrcs] = pin;
+      zdst[k - nSrcs] = pin ? a.devicePointer : nullptr;
     }
-    if (k < nSrcs) zsrc[k] = a.devicePointer;
-    else zdst[k - nSrcs] = a.devicePointer;
+    nPinned += pin ? 1 : 0;
   }
-  if (pinned) {
+  if (nPinned == nSrcs + nDsts) {
     r = reduceCopyDevice(nSrcs, zsrc, nDsts, zdst, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs,
                          nullptr, postOp, s);
     if (r != nexrSuccess) return r;
     NEXR_HIP(hipStreamSynchronize(s));
     return nexrSuccess;
   }
-  // Pageable memory: staged through device memory in a two-stream chunk pipeline.
+  // Some buffers pageable: a two-stream chunk pipeline through device memory for those only; the
+  // pinned ones (e.g. the emulated transport's FIFOs) are read and written in place by the kernel.
   const size_t esz = typeSize(datatype);
   static const long chunkOverride = envLong("NEXR_HOST_CHUNK_BYTES", 8l << 20);
   size_t chunkElts = ((size_t)(chunkOverride > 4096 ? chunkOverride : 4096) / esz) & ~(size_t)15;
@@ -379,6 +385,8 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
   HostStage* st = nullptr;
   r = stageFor(chunkBytes * (size_t)(nSrcs + 1), &st);
   if (r != nexrSuccess) return r;
+  bool anyPageableDst = false;
+  for (int d = 0; d < nDsts; d++) anyPageableDst |= !pdst[d];
   const size_t nChunks = (nElts + chunkElts - 1) / chunkElts;
   for (size_t c = 0; c < nChunks; c++) {
     const int slot = (int)(c & 1);
@@ -388,17 +396,27 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
     if (c >= 2) NEXR_HIP(hipStreamWaitEvent(s, st->outDone[slot], 0));  // slot drained by chunk c-2's D2H
     const void* dsrc[NEXR_MAX_SRCS];
     for (int k = 0; k < nSrcs; k++) {
+      if (psrc[k]) {
+        dsrc[k] = (const char*)zsrc[k] + e0 * esz;
+        continue;
+      }
       dsrc[k] = base + chunkBytes * k;
       NEXR_HIP(hipMemcpyAsync((void*)dsrc[k], (const char*)srcs[k] + e0 * esz, n * esz, hipMemcpyHostToDevice, s));
     }
-    void* ddst[1] = {base + chunkBytes * nSrcs};
-    r = reduceCopyDevice(nSrcs, dsrc, 1, ddst, n, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs, nullptr,
+    void* ddst[NEXR_MAX_DSTS + 1];
+    int m = 0;
+    for (int d = 0; d < nDsts; d++)
+      if (pdst[d]) ddst[m++] = (char*)zdst[d] + e0 * esz;
+    char* staged = base + chunkBytes * nSrcs;
+    if (anyPageableDst) ddst[m++] = staged;
+    r = reduceCopyDevice(nSrcs, dsrc, m, ddst, n, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs, nullptr,
                          postOp, s);
     if (r != nexrSuccess) return r;
     NEXR_HIP(hipEventRecord(st->kernelDone[slot], s));
     NEXR_HIP(hipStreamWaitEvent(st->out, st->kernelDone[slot], 0));
     for (int d = 0; d < nDsts; d++)
-      NEXR_HIP(hipMemcpyAsync((char*)dsts[d] + e0 * esz, ddst[0], n * esz, hipMemcpyDeviceToHost, st->out));
+      if (!pdst[d])
+        NEXR_HIP(hipMemcpyAsync((char*)dsts[d] + e0 * esz, staged, n * esz, hipMemcpyDeviceToHost, st->out));
     NEXR_HIP(hipEventRecord(st->outDone[slot], st->out));
   }
   NEXR_HIP(hipStreamSynchronize(st->out));

@@ -48,6 +48,7 @@ struct Conn {
   size_t slotBytes = 0;  // bytes per FIFO step; 0 = the communicator's stepBytes (P2P links: p2pChunkSize)
   int device = 0;        // device of the FIFO (device memory mode)
   bool ownsFifo = true;  // false for a peer process's FIFO mapped over IPC
+  bool pinned = false;   // host-memory FIFO from hipHostMalloc
   ConnState own;
   ConnState* st = &own;  // the counters: `own` for thread ranks, a shared-memory slot for process ranks
   // Each endpoint's step (the conn->step a Primitives loads and saves, prims_simple.h:528-560): only
@@ -668,12 +669,28 @@ nexrResult_t runThreads(nexrRingComm* c, Shared& sh, const std::vector<std::func
   return nexrSuccess;
 }
 
+// NEXR_RING_HOST_PINNED=0 keeps host-memory FIFOs pageable (the staged path for every step).
+bool pinnedHostFifos() {
+  static const bool on = [] {
+    const char* e = getenv("NEXR_RING_HOST_PINNED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes = 0) {
   k->device = device;
   if (bytes == 0) bytes = c->cfg.buffBytes;
   if (c->cfg.memMode == nexrRingDeviceMemory) {
     if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, bytes) != hipSuccess)
       return nexrUnhandledCudaError;
+  } else if (c->needHip && pinnedHostFifos()) {
+    // Host memory with the MI355X doing the steps: pinned, device-mapped FIFOs, so that a step whose
+    // user buffers are pinned too runs as one zero-copy kernel over PCIe (nexrReduceCopyHost) instead
+    // of staging every slice through device memory.
+    if (hipHostMalloc((void**)&k->fifo, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+      return nexrUnhandledCudaError;
+    k->pinned = true;
   } else {
     k->fifo = (char*)aligned_alloc(4096, bytes);
     if (!k->fifo) return nexrSystemError;
@@ -751,6 +768,8 @@ void freeConn(nexrRingComm* c, Conn* k) {
     if (c->cfg.memMode == nexrRingDeviceMemory) {
       (void)hipSetDevice(k->device);
       (void)hipFree(k->fifo);
+    } else if (k->pinned) {
+      (void)hipHostFree(k->fifo);
     } else {
       free(k->fifo);
     }

@@ -347,6 +347,35 @@ def test_host_zero_copy_pinned_buffers(nexr, oracle, dev):
     assert same(mg.F16, pageable, exp)
 
 
+@pytest.mark.parametrize("mask", [0b00001, 0b00110, 0b01011, 0b10000, 0b11100, 0b01111, 0b10101])
+def test_host_partially_pinned_buffers(nexr, oracle, dev, mask):
+    """Pinned and pageable host buffers in one call (e.g. pinned FIFOs beside pageable user buffers):
+    the kernel reads/writes the pinned ones in place and only the pageable ones are staged. Bit i of
+    `mask` pins buffer i of [src0, src1, src2, dst0, dst1]; 3 chunks of 8 MiB plus a ragged one."""
+    n = 6_000_011
+    dt = mg.F32
+    srcs = mg.gen_inputs(dt, 3, n, 900 + mask, special=True)
+    exp = oracle.reduce_copy(srcs, 1, dt, mg.SUM, threads=16)[0]
+    bufs, keep = [], []
+    for i in range(5):
+        if mask >> i & 1:
+            t = torch.zeros(n, dtype=torch.float32).pin_memory()
+            if i < 3:
+                t.copy_(torch.from_numpy(srcs[i]))
+            keep.append(t)
+            bufs.append((t.data_ptr(), lambda t=t: t.numpy()))
+        else:
+            a = srcs[i].copy() if i < 3 else np.zeros(n, np.float32)
+            keep.append(a)
+            bufs.append((a.ctypes.data, lambda a=a: a))
+    nexr.reduce_copy_ptrs([b[0] for b in bufs[:3]], [b[0] for b in bufs[3:]], n, dt, mg.SUM, host=True)
+    for b in bufs[3:]:
+        assert same(dt, b[1](), exp)
+    # in place on src0, whatever its kind
+    nexr.reduce_copy_ptrs([b[0] for b in bufs[:3]], [bufs[0][0]], n, dt, mg.SUM, host=True)
+    assert same(dt, bufs[0][1](), exp)
+
+
 def test_random_fuzz_against_oracle(nexr, oracle, dev):
     # 300 random (datatype, op, K, M, n, per-pointer offsets, pre/post) cases, special values on
     rng = np.random.default_rng(20261015)

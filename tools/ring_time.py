@@ -25,6 +25,7 @@ ORACLE_FNS = (cast(L.oracle_reduce_copy_fn), cast(L.oracle_reduce_copy_ll_fn), c
 def run(n, mode_name, proto_name, coll, iters):
     proto = {"simple": ring.PROTO_SIMPLE, "ll": ring.PROTO_LL, "ll128": ring.PROTO_LL128}[proto_name]
     mode = ring.DEVICE_MEMORY if mode_name == "device" else ring.HOST_MEMORY
+    pinned = mode_name == "host-pinned"
     rng = np.random.default_rng(n)
     # small integers: every sum order gives the same fp32 result, so numpy checks the schedule
     x = [rng.integers(-1000, 1000, count * n).astype(np.float32) for _ in range(n)]
@@ -36,6 +37,10 @@ def run(n, mode_name, proto_name, coll, iters):
         recv = [torch.zeros(out_n, dtype=torch.float32, device="cuda") for _ in range(n)]
         sp, rp = [t.data_ptr() for t in send], [t.data_ptr() for t in recv]
         torch.cuda.synchronize()
+    elif pinned:  # page-locked user buffers: with the pinned FIFOs every step is one zero-copy kernel
+        send = [torch.from_numpy(v).pin_memory() for v in x]
+        recv = [torch.zeros(out_n, dtype=torch.float32).pin_memory() for _ in range(n)]
+        sp, rp = [t.data_ptr() for t in send], [t.data_ptr() for t in recv]
     else:
         send, recv = x, [np.zeros(out_n, np.float32) for _ in range(n)]
         sp, rp = [v.ctypes.data for v in send], [v.ctypes.data for v in recv]
@@ -70,8 +75,8 @@ def run(n, mode_name, proto_name, coll, iters):
 
 print(f"{'ranks':>5} {'mode':<10} {'proto':<6} {'collective':<14} {'ms/call':>9} {'algbw GB/s':>11}")
 for n in [int(v) for v in os.environ.get("RING_TIME_RANKS", "2,4").split(",")]:
-    modes = os.environ.get("RING_TIME_MODES", "cpu-oracle,host,device").split(",")
-    for mode_name, protos in (("cpu-oracle", ("simple",)), ("host", ("simple",)),
+    modes = os.environ.get("RING_TIME_MODES", "cpu-oracle,host,host-pinned,device").split(",")
+    for mode_name, protos in (("cpu-oracle", ("simple",)), ("host", ("simple",)), ("host-pinned", ("simple",)),
                               ("device", ("simple", "ll", "ll128"))):
         if mode_name not in modes:
             continue
