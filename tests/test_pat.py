@@ -202,3 +202,22 @@ def test_pat_one_rank_empty_and_rejections(ring, fn, nexr):
         assert e.value.code == nexr.Result.InvalidUsage
     with pytest.raises(nexr.NexrError):
         ring.pat_schedule(True, 1, 0, 10, mg.F32)
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3, 4, 8])
+def test_in_place_reduce_scatter_ring_and_pat(ring, oracle, fn, n_ranks):
+    """ncclReduceScatter in place: recvbuff = sendbuff + rank*recvcount (the rank's own segment)."""
+    from oracle import pat
+    from oracle.ring import reduce_scatter_expected
+    recvcount, buff, dt = 3_001, 8 * 1024, mg.F32
+    inputs = mg.gen_inputs(dt, n_ranks, recvcount * n_ranks, 0x1A + n_ranks, False)
+    for kind in ("ring", "pat"):
+        bufs = [x.copy() for x in inputs]
+        with _comm(ring, fn, n_ranks, buff) as comm:
+            recv = [b[r * recvcount:] for r, b in enumerate(bufs)]
+            (comm.reduce_scatter if kind == "ring" else comm.pat_reduce_scatter)(_ptrs(bufs), _ptrs(recv), recvcount,
+                                                                                  dt, 0)
+        exp = (reduce_scatter_expected(inputs, dt, 0) if kind == "ring"
+               else pat.reduce_scatter_expected(inputs, dt, 0, 0, buff // 8))
+        for r in range(n_ranks):
+            assert bufs[r][r * recvcount:(r + 1) * recvcount].tobytes() == exp[r].tobytes(), (kind, r)
