@@ -1,0 +1,375 @@
+// nexr_emu.h — internal to the CPU-emulated collectives (nexr_ring.cpp, nexr_pat.cpp, nexr_p2p.cpp):
+// the connection and FIFO state, the communicator, and the host-side Primitives every schedule
+// drives. Not installed; the public surface is include/nexr_ring.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <thread>
+#include <vector>
+
+#include "../../include/nexr_ring.h"
+
+namespace nexr_emu {
+
+constexpr int kSteps = 8;                                // NCCL_STEPS (src/include/device.h:649)
+constexpr int kMaxArity = 3;                             // NCCL_MAX_TREE_ARITY (device.h:185)
+constexpr size_t kDefaultBuffBytes = 4u << 20;           // NCCL_BUFFSIZE default (init.cc:620-634)
+constexpr size_t kDefaultLLBuffBytes = 8 * 512 * kSteps * 16;  // DEFAULT_LL_BUFFSIZE (init.cc:618)
+constexpr size_t kDefaultLL128BuffBytes = 120 * 640 * kSteps * 8;  // DEFAULT_LL128_BUFFSIZE (init.cc:619)
+constexpr size_t kMinBuffBytes = kSteps * 512;           // one SIMPLE grain per step at least
+
+// ProtoSimple<SlicePerChunk = chunkSteps/sliceSteps, StepPerSlice = sliceSteps> of a collective
+// (src/include/collectives.h:16-25); LL and LL128 move one step per primitive call.
+struct Geom {
+  int chunkSteps, sliceSteps;
+};
+constexpr Geom kGeomRing{kSteps / 2, kSteps / 4};  // ALLREDUCE/ALLGATHER/REDUCESCATTER_*STEPS
+constexpr Geom kGeomPipe{1, 1};                    // BROADCAST/REDUCE_*STEPS; the tree's ProtoSimple<1,1>
+
+// One directed connection. The FIFO belongs to the receiver (the sender writes into it, like a
+// P2P/SHM transport's recv buffer, src/include/device.h:753-771).
+struct ConnState {
+  alignas(64) std::atomic<uint64_t> tail{0};  // steps published by the sender   (postPeer, Send)
+  alignas(64) std::atomic<uint64_t> head{0};  // steps released by the receiver  (postPeer, Recv)
+};
+struct Conn {
+  char* fifo = nullptr;
+  size_t slotBytes = 0;  // bytes per FIFO step; 0 = the communicator's stepBytes (P2P links: p2pChunkSize)
+  int device = 0;        // device of the FIFO (device memory mode)
+  bool ownsFifo = true;  // false for a peer process's FIFO mapped over IPC
+  bool pinned = false;   // host-memory FIFO from hipHostMalloc
+  ConnState own;
+  ConnState* st = &own;  // the counters: `own` for thread ranks, a shared-memory slot for process ranks
+  // Each endpoint's step (the conn->step a Primitives loads and saves, prims_simple.h:528-560): only
+  // the sending thread touches sendStep and only the receiving thread touches recvStep.
+  alignas(64) uint64_t sendStep = 0;
+  alignas(64) uint64_t recvStep = 0;
+};
+
+// Process ranks (nexrPeerRingCommCreate): one POSIX shared-memory segment per communicator holds
+// the rendezvous, every connection's head/tail counters and a common abort word. Slot r belongs to
+// rank r: its FIFO's IPC handle and the counters of the connection INTO rank r.
+constexpr uint32_t kPeerMagic = 0x6e657872u;  // "nexr"
+struct alignas(64) PeerHeader {
+  std::atomic<uint32_t> initState;  // 0 fresh, 1 being configured, 2 configured
+  std::atomic<uint32_t> joined;
+  std::atomic<uint32_t> left;
+  std::atomic<uint32_t> abort;
+  std::atomic<uint32_t> patJoined;  // ranks that published their PAT receive FIFOs
+  std::atomic<uint32_t> p2pJoined;  // ranks that published their P2P receive FIFOs
+  uint32_t magic, nRanks, protocol, pad;
+  uint64_t buffBytes;
+};
+struct PeerSlot {
+  hipIpcMemHandle_t fifoHandle;
+  alignas(64) ConnState conn;
+};
+// Links beyond the ring for PAT (r -> r +- 2^d) and P2P (any r -> q), one per ordered pair: the
+// receiver's FIFO handles and the link's counters. Only for communicators of up to kPeerLinkMaxRanks.
+constexpr int kPeerLinkMaxRanks = 64;
+struct PeerLink {
+  hipIpcMemHandle_t patFifo, p2pFifo, p2pLLFifo;
+  alignas(64) ConnState pat;
+  alignas(64) ConnState p2p;
+  alignas(64) ConnState p2pLL;
+};
+inline size_t peerShmBytes(int n) {
+  return sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot) +
+         (n <= kPeerLinkMaxRanks ? (size_t)n * n * sizeof(PeerLink) : 0);
+}
+inline PeerHeader* peerHeader(void* base) { return (PeerHeader*)base; }
+inline PeerSlot* peerSlot(void* base, int r) { return (PeerSlot*)((char*)base + sizeof(PeerHeader)) + r; }
+inline PeerLink* peerLink(void* base, int n, int from, int to) {
+  return (PeerLink*)((char*)base + sizeof(PeerHeader) + (size_t)n * sizeof(PeerSlot)) + (size_t)from * n + to;
+}
+
+inline int64_t divUp(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t alignUp(int64_t a, int64_t b) { return divUp(a, b) * b; }
+
+struct TreeLinks {
+  int up = -1;
+  int down[kMaxArity] = {-1, -1, -1};
+  int nDown() const {
+    int k = 0;
+    while (k < kMaxArity && down[k] >= 0) k++;
+    return k;
+  }
+};
+
+}  // namespace nexr_emu
+
+using namespace nexr_emu;
+
+struct nexrRingComm {
+  nexrRingConfig cfg;
+  size_t stepBytes = 0;
+  std::vector<Conn*> conns;     // ring: conns[r] is the connection into rank r from rank r-1
+  std::vector<TreeLinks> tree;  // tree topology (computed at creation)
+  std::vector<Conn*> treeUp;    // treeUp[r]: r -> parent(r) (reduce); created by the first tree call
+  std::vector<Conn*> treeDown;  // treeDown[r]: parent(r) -> r (broadcast)
+  std::vector<Conn*> patConns;  // PAT: patConns[from*nRanks+to] for to = from +- 2^d (ring link excluded)
+  std::vector<Conn*> p2pConns;  // ncclSend/ncclRecv: p2pConns[from*nRanks+to] (connIndex 1), made on first use
+  std::vector<Conn*> p2pLLConns;  // the same links' LL buffers, for messages <= 16 KiB
+  size_t p2pChunkBytes = 0;     // comm->p2pChunkSize
+  std::vector<int> devices;
+  std::vector<hipStream_t> streams, streams2;  // streams2: the tree's broadcast-half threads
+  std::vector<uint32_t*> status, status2;      // LL: pinned status words the kernel reports timeouts in
+  bool ll = false;     // LL or LL128: one FIFO step per primitive call, data readiness in line flags
+  int proto = nexrRingProtoSimple;
+  bool needHip = false;
+  bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
+  bool broken = false;
+  // Process ranks: this process is rank `self` only.
+  bool peer = false;
+  int self = 0;
+  void* shm = nullptr;
+  size_t shmBytes = 0;
+  char shmName[256] = {0};
+};
+
+namespace nexr_emu {
+
+struct Shared {
+  std::atomic<bool> abort{false};
+  std::atomic<int> firstError{0};
+  std::atomic<uint32_t>* remoteAbort = nullptr;  // process ranks: the communicator-wide abort word
+  void fail(nexrResult_t r) {
+    int expected = 0;
+    firstError.compare_exchange_strong(expected, (int)r);
+    abort.store(true);
+    if (remoteAbort) remoteAbort->store(1, std::memory_order_release);
+  }
+  bool aborted() const {
+    return abort.load(std::memory_order_relaxed) || (remoteAbort && remoteAbort->load(std::memory_order_acquire));
+  }
+};
+
+enum { kNone = -1, kInput = 0, kOutput = 1 };  // SrcBuf / DstBuf of genericOp
+
+// One rank's Primitives<T, RedOp, Fan, Direct, Proto> (prims_simple.h / prims_ll.h / prims_ll128.h),
+// host side: up to kMaxArity recv peers and kMaxArity send peers (FanAsymmetric of the tree).
+struct Prims {
+  nexrRingComm* c;
+  Shared* sh;
+  int rank;
+  Conn* recv[kMaxArity];
+  int nRecv = 0;
+  Conn* send[kMaxArity];
+  int nSend = 0;
+  const char* userInput;
+  char* userOutput;
+  size_t esz;
+  int64_t stepSize;  // elements per FIFO step (prims_simple.h:607)
+  int stepPerSlice = 1, slicePerChunk = 1;
+  int datatype, devOp;
+  uint64_t redOpArgs[1];
+  nexrReduceCopyFn fn;
+  nexrReduceCopyLLFn llFn;
+  nexrReduceCopyLL128Fn ll128Fn;
+  uint32_t* status;
+  hipStream_t stream;
+  bool device;
+  int proto = nexrRingProtoSimple;  // the communicator's, or LL for a small P2P message (sendrecv.h)
+
+  char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
+  size_t slot(const Conn* q) const { return q->slotBytes ? q->slotBytes : c->stepBytes; }
+
+  // loadRecvConn / loadSendConn (prims_simple.h:512-513, :557-558): a SIMPLE Primitives starts each
+  // connection at step roundUp(conn->step, SlicePerChunk*StepPerSlice), so a collective with 2-step
+  // slices that follows one with 1-step slices (Broadcast, Reduce) never starts a slice in the last
+  // FIFO slot. Both endpoints of a connection hold the same step between collectives and round alike,
+  // and the receiver publishes its rounded step as head ("return credits in case we rounded up",
+  // :514-517): the steps skipped by rounding were never sent, so the sender must not wait for them.
+  void attach() {
+    if (proto != nexrRingProtoSimple) return;
+    const uint64_t cs = (uint64_t)(stepPerSlice * slicePerChunk);
+    for (int i = 0; i < nRecv; i++) {
+      recv[i]->recvStep = (recv[i]->recvStep + cs - 1) / cs * cs;
+      recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
+    }
+    for (int i = 0; i < nSend; i++) send[i]->sendStep = (send[i]->sendStep + cs - 1) / cs * cs;
+  }
+
+  // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
+  // abortable like checkAbort (primitives.h:142-156).
+  bool waitAtLeast(std::atomic<uint64_t>& a, uint64_t target) {
+    if (a.load(std::memory_order_acquire) >= target) return true;
+    const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+    auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 0;; spins++) {
+      if (a.load(std::memory_order_acquire) >= target) return true;
+      if (sh->aborted()) {
+        sh->fail(nexrRemoteError);
+        return false;
+      }
+      if ((spins & 1023) == 0 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) {
+        sh->fail(nexrInternalError);
+        return false;
+      }
+      std::this_thread::yield();
+    }
+  }
+
+  // genericOp<DirectRecv=0, DirectSend=0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330),
+  // with the non-direct FIFO pointers (waitPeer :150-164 default branch). srcs = [user src, recv
+  // peers...], dsts = [user dst, send peers...] (:131-132, :238-242).
+  bool genericOp(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t nelem,
+                 bool postOp) {
+    const int nr = Recv ? nRecv : 0, ns = Send ? nSend : 0;
+    nelem = nelem < 0 ? 0 : nelem;
+    int64_t sliceSize = stepSize * stepPerSlice;
+    sliceSize = std::max(divUp(nelem, 16 * slicePerChunk) * 16, sliceSize / 32);
+    int64_t offset = 0;
+    for (int slice = 0; slice < slicePerChunk; slice++) {
+      sliceSize = std::min(sliceSize, nelem - offset);
+      if (sliceSize < 0) sliceSize = 0;
+      const void* srcs[1 + kMaxArity];
+      void* dsts[1 + kMaxArity];
+      int k = 0, m = 0;
+      if (srcBuf != kNone) srcs[k++] = buf(srcBuf) + (srcIx + offset) * esz;
+      if (dstBuf != kNone) dsts[m++] = buf(dstBuf) + (dstIx + offset) * esz;
+      for (int i = 0; i < nr; i++) {  // wait for the peer's data: tail >= step + StepPerSlice
+        Conn* q = recv[i];
+        if (!waitAtLeast(q->st->tail, q->recvStep + stepPerSlice)) return false;
+        srcs[k++] = q->fifo + (q->recvStep % kSteps) * slot(q);
+      }
+      for (int i = 0; i < ns; i++) {  // wait for credit: head + NCCL_STEPS >= step + StepPerSlice
+        Conn* q = send[i];
+        if (q->sendStep + stepPerSlice > (uint64_t)kSteps &&
+            !waitAtLeast(q->st->head, q->sendStep + stepPerSlice - kSteps))
+          return false;
+        dsts[m++] = q->fifo + (q->sendStep % kSteps) * slot(q);
+      }
+      if (sliceSize > 0 && k > 0 && m > 0) {
+        // PreOpSrcs = SrcBuf != Input ? 0 : 1 (prims_simple.h:279-280); preOpArgs = redOpArgs.
+        const int nPre = srcBuf == kInput ? 1 : 0;
+        nexrResult_t r = fn(k, srcs, m, dsts, (size_t)sliceSize, datatype, devOp, redOpArgs[0], nPre,
+                            nPre ? redOpArgs : nullptr, postOp ? 1 : 0, (nexrStream_t)stream);
+        if (r == nexrSuccess && device) {
+          hipError_t e = hipStreamSynchronize(stream);  // data complete before the step is posted
+          if (e != hipSuccess) r = nexrUnhandledCudaError;
+        }
+        if (r != nexrSuccess) {
+          sh->fail(r);
+          return false;
+        }
+      }
+      // postPeer (prims_simple.h:177-188): release the slot / publish the data.
+      for (int i = 0; i < nr; i++) {
+        recv[i]->recvStep += stepPerSlice;
+        recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
+      }
+      for (int i = 0; i < ns; i++) {
+        send[i]->sendStep += stepPerSlice;
+        send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
+      }
+      offset += sliceSize;
+    }
+    return true;
+  }
+  // LLGenericOp<RECV, SEND, SrcBuf, DstBuf> (prims_ll.h:218-283) / GenericOp of prims_ll128.h
+  // (:294-331): one FIFO step per call. The sender waits for a credit (waitSend :55-75); the
+  // receiver's data readiness is the line flags (NCCL_LL_FLAG(step+1), :42-43; step+1 for LL128).
+  // The host additionally waits for the sender's step so that the kernel's flag poll succeeds at
+  // once: two emulated ranks may share one GPU, and a kernel spinning on a producer that cannot be
+  // scheduled beside it must never be launched.
+  bool genericOpLL(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t nelem,
+                   bool postOp) {
+    const int nr = Recv ? nRecv : 0, ns = Send ? nSend : 0;
+    nelem = nelem < 0 ? 0 : nelem;
+    for (int i = 0; i < ns; i++) {
+      Conn* q = send[i];
+      if (q->sendStep + 1 > (uint64_t)kSteps && !waitAtLeast(q->st->head, q->sendStep + 1 - kSteps)) return false;
+    }
+    for (int i = 0; i < nr; i++)
+      if (!waitAtLeast(recv[i]->st->tail, recv[i]->recvStep + 1)) return false;
+    if (nelem > 0) {
+      const void* recvLines[kMaxArity];
+      void* sendLines[kMaxArity];
+      uint32_t rf32[kMaxArity], sf32[kMaxArity];
+      uint64_t rf64[kMaxArity], sf64[kMaxArity];
+      for (int i = 0; i < nr; i++) {
+        recvLines[i] = recv[i]->fifo + (recv[i]->recvStep % kSteps) * slot(recv[i]);
+        rf64[i] = recv[i]->recvStep + 1;
+        rf32[i] = (uint32_t)rf64[i];
+      }
+      for (int i = 0; i < ns; i++) {
+        sendLines[i] = send[i]->fifo + (send[i]->sendStep % kSteps) * slot(send[i]);
+        sf64[i] = send[i]->sendStep + 1;
+        sf32[i] = (uint32_t)sf64[i];
+      }
+      const void* src = srcBuf != kNone ? buf(srcBuf) + srcIx * esz : nullptr;
+      void* dst = dstBuf != kNone ? buf(dstBuf) + dstIx * esz : nullptr;
+      const int srcIsInput = srcBuf == kInput ? 1 : 0;
+      if (status) *status = 0;
+      const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
+      nexrResult_t r;
+      if (proto == nexrRingProtoLL128)
+        r = ll128Fn(src, srcIsInput, nr, recvLines, rf64, dst, ns, sendLines, sf64, (size_t)nelem, datatype, devOp,
+                    redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
+      else
+        r = llFn(src, srcIsInput, nr, recvLines, rf32, dst, ns, sendLines, sf32, (size_t)nelem, datatype, devOp,
+                 redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
+      if (r == nexrSuccess && device && hipStreamSynchronize(stream) != hipSuccess) r = nexrUnhandledCudaError;
+      if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
+      if (r != nexrSuccess) {
+        sh->fail(r);
+        return false;
+      }
+    }
+    for (int i = 0; i < nr; i++) {  // postRecv (:80-83)
+      recv[i]->recvStep += 1;
+      recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
+    }
+    for (int i = 0; i < ns; i++) {  // incSend (:85-93); the flag-wrap cleanup at NCCL_LL_CLEAN_MASK needs ~2^31 steps
+      send[i]->sendStep += 1;
+      send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
+    }
+    return true;
+  }
+  bool op(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t n, bool postOp) {
+    return proto != nexrRingProtoSimple ? genericOpLL(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp)
+                 : genericOp(Recv, Send, srcBuf, dstBuf, srcIx, dstIx, n, postOp);
+  }
+  // The primitives the schedules use (prims_simple.h:897-976; the direct* forms reduce to these
+  // without registered peer buffers).
+  bool sendInput(int64_t inpIx, int64_t n) { return op(false, true, kInput, kNone, inpIx, -1, n, false); }
+  bool copySend(int64_t inpIx, int64_t outIx, int64_t n) { return op(false, true, kInput, kOutput, inpIx, outIx, n, false); }
+  bool sendFromOutput(int64_t outIx, int64_t n) { return op(false, true, kOutput, kNone, outIx, -1, n, false); }
+  bool recvReduceSend(int64_t inpIx, int64_t n) { return op(true, true, kInput, kNone, inpIx, -1, n, false); }
+  bool recvReduceCopy(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
+    return op(true, false, kInput, kOutput, inpIx, outIx, n, postOp);
+  }
+  bool recvReduceCopySend(int64_t inpIx, int64_t outIx, int64_t n, bool postOp) {
+    return op(true, true, kInput, kOutput, inpIx, outIx, n, postOp);
+  }
+  bool recvCopySend(int64_t outIx, int64_t n) { return op(true, true, kNone, kOutput, -1, outIx, n, false); }
+  bool recvOutput(int64_t outIx, int64_t n) { return op(true, false, kNone, kOutput, -1, outIx, n, false); }
+};
+
+// ---- shared helpers (nexr_ring.cpp) ----------------------------------------------------------------
+nexrResult_t defaultLLFn(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
+                         const uint32_t* recvFlags, void* dst, int nSend, void* const* sendLines,
+                         const uint32_t* sendFlags, size_t n, int dt, int op, uint64_t arg, int post, uint32_t* status,
+                         uint32_t timeoutUs, nexrStream_t s);
+Prims makePrims(nexrRingComm* c, Shared* sh, int rank, const void* sendbuff, void* recvbuff, size_t esz, int datatype,
+                const nexrDevRedOpFull& red, Geom g, hipStream_t stream, uint32_t* status);
+nexrResult_t oneRank(nexrRingComm* c, int r, const void* sendbuff, void* recvbuff, size_t count, int datatype,
+                     const nexrDevRedOpFull& red, size_t esz);
+nexrResult_t prepare(nexrRingComm* c, int datatype, int op, size_t* esz, nexrDevRedOpFull* red);
+nexrResult_t runThreads(nexrRingComm* c, Shared& sh, const std::vector<std::function<void()>>& jobs);
+nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes = 0);
+nexrResult_t enablePeer(int a, int b);
+nexrResult_t ensureSecondStreams(nexrRingComm* c);
+// Process ranks: connect this rank's PAT (p2p = false) or P2P links on first use (collective).
+nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p);
+nexrResult_t peerFinish(nexrRingComm* c, Shared& sh);
+
+}  // namespace nexr_emu
