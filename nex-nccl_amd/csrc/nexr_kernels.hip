@@ -53,6 +53,20 @@ struct Fold {
   }
   // in[s] = the K loaded packs of one position
   __device__ __forceinline__ u32x4 run(const u32x4 (&in)[K]) const {
+    if constexpr ((D == nexrInt8 || D == nexrUint8) && K >= 2 &&
+                  (OP == nexrDevSum || OP == nexrDevProd || OP == nexrDevMinMax)) {
+      using F = Fold8<OP, D == nexrInt8, IsMin>;  // two bytes per packed 16-bit instruction
+      u16x8 ae, ao;
+      F::split(in[0], ae, ao);
+#pragma unroll
+      for (int s = 1; s < K; s++) {
+        u16x8 e, o;
+        F::split(in[s], e, o);
+        ae = F::step(ae, e);
+        ao = F::step(ao, o);
+      }
+      return F::join(ae, ao);
+    }
     V acc = pre(bc<V>(in[0]), 0);
 #pragma unroll
     for (int s = 1; s < K; s++) acc = reduce_step<D, OP, IsMin>(acc, pre(bc<V>(in[s]), s));

@@ -208,4 +208,49 @@ __device__ __forceinline__ typename Ty<D>::V reduce_step(typename Ty<D>::V acc, 
   else return T::add(acc, v);  // Sum, PreMulSum, SumPostDiv all reduce with ncclAdd (:437-496)
 }
 
+// 8-bit packs, two bytes per 16-bit lane, so that one packed 16-bit instruction
+// (v_pk_{add,mul_lo}_u16, v_pk_{min,max}_{i16,u16}) folds two bytes; the fold stays in this form
+// across all K sources and is packed back once. Bit-identical to the byte-wise fold:
+//   Sum/Prod: even bytes in the LOW byte of each lane with the odd byte above it as don't-care, odd
+//     bytes shifted down: the low byte of a 16-bit sum or product depends only on the operands' low
+//     bytes, which is ncclAdd / ncclMultiply on the unsigned byte (wrap mod 2^8).
+//   Min/Max: every byte in the HIGH byte of a lane over a zero low byte: 16-bit order (signed for
+//     int8, unsigned for uint8) is then exactly the byte's order, with no sign extension.
+template <int OP, bool Signed, bool IsMin>
+struct Fold8 {
+  static constexpr bool kHigh = OP == nexrDevMinMax;
+  __device__ static __forceinline__ void split(u32x4 x, u16x8& ev, u16x8& od) {
+    const u16x8 h = bc<u16x8>(x);
+    if constexpr (kHigh) {
+      ev = h << 8;
+      od = h & (u16x8)0xff00;
+    } else {
+      ev = h;
+      od = h >> 8;
+    }
+  }
+  __device__ static __forceinline__ u16x8 step(u16x8 c, u16x8 v) {
+    if constexpr (OP == nexrDevProd) {
+      return c * v;
+    } else if constexpr (OP == nexrDevMinMax && Signed) {
+      return bc<u16x8>(IsMin ? __builtin_elementwise_min(bc<i16x8>(c), bc<i16x8>(v))
+                             : __builtin_elementwise_max(bc<i16x8>(c), bc<i16x8>(v)));
+    } else if constexpr (OP == nexrDevMinMax) {
+      return IsMin ? __builtin_elementwise_min(c, v) : __builtin_elementwise_max(c, v);
+    } else {
+      return c + v;
+    }
+  }
+  // result byte 2i from the even lane i, byte 2i+1 from the odd lane i (v_perm_b32: bytes 0-3 select
+  // from the second operand, 4-7 from the first)
+  __device__ static __forceinline__ u32x4 join(u16x8 ev, u16x8 od) {
+    const u32x4 e = bc<u32x4>(ev), o = bc<u32x4>(od);
+    constexpr uint32_t sel = kHigh ? 0x07030501u : 0x06020400u;
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = __builtin_amdgcn_perm(o[i], e[i], sel);
+    return r;
+  }
+};
+
 }  // namespace nexr
