@@ -103,9 +103,12 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 // Steady-state sweeps over U in {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8
 // (tools/tune_kernel.hip, tools/tune_sched.hip TUNE_MODE=geom; profiles/r01_tune_*.log,
 // r01_skew.log, r01s2_geom_*.log): U = 4, B = 256 is best or within noise of best everywhere except
-// fp16 with K = 8, where U = 1, B = 1024 (16 waves) is 1.7-2.8 % faster in three separate runs.
+// the 16-bit floats with K = 8, where U = 1, B = 1024 (16 waves) is faster: fp16 399.9 vs 407.9 us,
+// bf16 394.9 vs 402.0 us in same-box A/Bs alternated six times (profiles/r01s3_*_geometry_ab.txt).
 constexpr int kTripPacks = 1024;
-__host__ __device__ constexpr int unroll_for(int dt, int k) { return dt == nexrFloat16 && k >= 8 ? 1 : 4; }
+__host__ __device__ constexpr int unroll_for(int dt, int k) {
+  return (dt == nexrFloat16 || dt == nexrBfloat16) && k >= 8 ? 1 : 4;
+}
 __host__ __device__ constexpr int block_for(int dt, int k) { return kTripPacks / unroll_for(dt, k); }
 
 }  // namespace nexr
