@@ -72,6 +72,12 @@ typedef struct {
   int treeRanksPerNode; /* tree topology: ranks per emulated node (0 = all ranks on one node, i.e. a
                            chain); must divide nRanks. Node heads form the double binary tree */
   int treeIndex;        /* which tree of the double binary tree: 0 (the btree) or 1 (mirror/shift) */
+  int nChannels;        /* channels (0 = 1, at most 64): every collective is split over them as the
+                           reference's planner splits it (src/enqueue.cc:539-690); each channel has
+                           its own links, FIFOs, streams and host threads and they run concurrently.
+                           Like the reference's duplicated channels (graph/connect.cc:146-160), the
+                           upper half of 2 or more channels uses the other tree of the double binary
+                           tree. Send/Recv always uses channel 0 */
 } nexrRingConfig;
 
 typedef struct nexrRingComm* nexrRingComm_t;

@@ -18,6 +18,7 @@
 namespace nexr_emu {
 
 constexpr int kSteps = 8;                                // NCCL_STEPS (src/include/device.h:649)
+constexpr int kMaxChannels = 64;                         // MAXCHANNELS (src/include/device.h:711)
 constexpr int kMaxArity = 3;                             // NCCL_MAX_TREE_ARITY (device.h:185)
 constexpr size_t kDefaultBuffBytes = 4u << 20;           // NCCL_BUFFSIZE default (init.cc:620-634)
 constexpr size_t kDefaultLLBuffBytes = 8 * 512 * kSteps * 16;  // DEFAULT_LL_BUFFSIZE (init.cc:618)
@@ -116,6 +117,9 @@ struct nexrRingComm {
   std::vector<Conn*> patConns;  // PAT: patConns[from*nRanks+to] for to = from +- 2^d (ring link excluded)
   std::vector<Conn*> p2pConns;  // ncclSend/ncclRecv: p2pConns[from*nRanks+to] (connIndex 1), made on first use
   std::vector<Conn*> p2pLLConns;  // the same links' LL buffers, for messages <= 16 KiB
+  // Channels 1..nChannels-1, each a communicator of its own (links, FIFOs, streams, tree) over the
+  // same ranks; channel 0 is this one. Only the top-level communicator is called by the API.
+  std::vector<nexrRingComm*> channels;
   size_t p2pChunkBytes = 0;     // comm->p2pChunkSize
   std::vector<int> devices;
   std::vector<hipStream_t> streams, streams2;  // streams2: the tree's broadcast-half threads
@@ -354,7 +358,19 @@ struct Prims {
   bool recvOutput(int64_t outIx, int64_t n) { return op(true, false, kNone, kOutput, -1, outIx, n, false); }
 };
 
+// One channel's share of a collective (ncclCollCbdPart, src/include/device.h:946-970): elements
+// [offset, offset + count) of every rank's buffers, moved in chunks of chunkCount elements.
+struct ChannelPart {
+  int channel;
+  int64_t offset, count, chunkCount;
+};
+inline nexrRingComm* channelComm(nexrRingComm* c, int k) { return k == 0 ? c : c->channels[(size_t)k - 1]; }
+
 // ---- shared helpers (nexr_ring.cpp) ----------------------------------------------------------------
+// The channels a collective of `count` elements uses and each one's part (scheduleCollTasksToPlan for
+// one task, src/enqueue.cc:539-690): trafficPerByte = ncclFuncTrafficPerByte (:74-81). chunkCount is
+// left 0 for the caller (calcCollChunking of each part).
+std::vector<ChannelPart> channelParts(const nexrRingComm* c, int64_t count, size_t esz, int trafficPerByte);
 nexrResult_t defaultLLFn(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
                          const uint32_t* recvFlags, void* dst, int nSend, void* const* sendLines,
                          const uint32_t* sendFlags, size_t n, int dt, int op, uint64_t arg, int post, uint32_t* status,

@@ -66,9 +66,11 @@ struct PatReduceScatterPlan : PatGeometry {
   int chunkCount, nelem = 0, rank, nranks;
   int lastA = 0, as = 0, a = 0, sendSkipped = 0, stepOffset = 0, scale = 1, phase = 0;
 
-  PatReduceScatterPlan(int chunkCount_, size_t esz, int64_t count_, int rank_, int nranks_)
-      : PatGeometry((uint64_t)chunkCount_ * esz, kSteps, kPatMaxParallel, (uint64_t)count_, esz, nranks_),
-        offset(0), end(count_), count(count_), chunkCount(chunkCount_), rank(rank_), nranks(nranks_) {
+  // The channel's part is [offset_, end_) of the `count_` elements per rank (reduce_scatter.h:100,
+  // all_gather.h:133: channelOffset, channelOffset + channelCount).
+  PatReduceScatterPlan(int chunkCount_, size_t esz, int64_t offset_, int64_t end_, int64_t count_, int rank_, int nranks_)
+      : PatGeometry((uint64_t)chunkCount_ * esz, kSteps, kPatMaxParallel, (uint64_t)(end_ - offset_), esz, nranks_),
+        offset(offset_), end(end_), count(count_), chunkCount(chunkCount_), rank(rank_), nranks(nranks_) {
     reset();
   }
   static int mirrorInvert(int i, int max) {
@@ -229,9 +231,11 @@ struct PatAllGatherPlan : PatGeometry {
   int asDim, v = 0;
   int bitCount[32], bitZeroStep[32];
 
-  PatAllGatherPlan(int chunkCount_, size_t esz, int64_t count_, int rank_, int nranks_)
-      : PatGeometry((uint64_t)chunkCount_ * esz, kSteps, kPatMaxParallel, (uint64_t)count_, esz, nranks_),
-        offset(0), end(count_), count(count_), chunkCount(chunkCount_), rank(rank_), nranks(nranks_) {
+  // The channel's part is [offset_, end_) of the `count_` elements per rank (reduce_scatter.h:100,
+  // all_gather.h:133: channelOffset, channelOffset + channelCount).
+  PatAllGatherPlan(int chunkCount_, size_t esz, int64_t offset_, int64_t end_, int64_t count_, int rank_, int nranks_)
+      : PatGeometry((uint64_t)chunkCount_ * esz, kSteps, kPatMaxParallel, (uint64_t)(end_ - offset_), esz, nranks_),
+        offset(offset_), end(end_), count(count_), chunkCount(chunkCount_), rank(rank_), nranks(nranks_) {
     asDim = log2Up(aggDelta);
     reset();
   }
@@ -509,12 +513,13 @@ struct PatRank {
     return true;
   }
 
-  void run(int64_t count, int nranks) {
-    const int64_t chunkCount = patChunkElems(p.c, p.esz, !reduceScatter, count);
+  void run(const ChannelPart& part, int64_t count, int nranks) {
+    const int chunkCount = (int)part.chunkCount;
+    const int64_t lo = part.offset, hi = part.offset + part.count;
     int pf = 1;
     const std::vector<PatOp> ops =
-        reduceScatter ? patOps(PatReduceScatterPlan((int)chunkCount, p.esz, count, p.rank, nranks), &pf)
-                      : patOps(PatAllGatherPlan((int)chunkCount, p.esz, count, p.rank, nranks), &pf);
+        reduceScatter ? patOps(PatReduceScatterPlan(chunkCount, p.esz, lo, hi, count, p.rank, nranks), &pf)
+                      : patOps(PatAllGatherPlan(chunkCount, p.esz, lo, hi, count, p.rank, nranks), &pf);
     // Worker group g runs ops g, g+pf, ... and stops after its first op with `last` set
     // (reduce_scatter.h:127-138): the stream must end on a whole batch whose every op is marked.
     for (size_t b = 0; b < ops.size(); b += (size_t)pf) {
@@ -558,7 +563,7 @@ nexrResult_t ensurePat(nexrRingComm* c) {
 
 // One rank's PAT collective on the calling thread (thread ranks and process ranks alike).
 void runPatRank(nexrRingComm* c, Shared* sh, int rank, bool reduceScatter, const void* sendbuff, void* recvbuff,
-                size_t count, size_t esz, int datatype, const nexrDevRedOpFull& red) {
+                size_t count, size_t esz, int datatype, const nexrDevRedOpFull& red, const ChannelPart& part) {
   const int n = c->cfg.nRanks;
   if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
   PatRank pr;
@@ -575,7 +580,7 @@ void runPatRank(nexrRingComm* c, Shared* sh, int rank, bool reduceScatter, const
     pr.sendDims[d].conn = patConn(c, rank, sendPeer);
     pr.sendDims[d].step = pr.sendDims[d].conn->sendStep;
   }
-  pr.run((int64_t)count, n);
+  pr.run(part, (int64_t)count, n);
 }
 
 // Argument checks shared by the thread-rank and process-rank PAT entry points.
@@ -604,17 +609,25 @@ nexrResult_t patCollective(nexrRingComm* c, bool reduceScatter, const void* cons
   for (int i = 0; i < n; i++)
     if (!sendbuffs[i] || !recvbuffs[i]) return nexrInvalidArgument;
   if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
-  r = ensurePat(c);
-  if (r != nexrSuccess) {
-    c->broken = true;
-    return r;
+  // split over the channels as any collective (ncclFuncTrafficPerByte = nRanks for both)
+  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, n);
+  for (ChannelPart& part : parts) {
+    nexrRingComm* ck = channelComm(c, part.channel);
+    r = ensurePat(ck);
+    if (r != nexrSuccess) {
+      c->broken = true;
+      return r;
+    }
+    part.chunkCount = patChunkElems(ck, esz, !reduceScatter, part.count);
   }
   Shared sh;
   std::vector<std::function<void()>> jobs;
-  for (int rank = 0; rank < n; rank++)
-    jobs.emplace_back([&, rank] {
-      runPatRank(c, &sh, rank, reduceScatter, sendbuffs[rank], recvbuffs[rank], count, esz, datatype, red);
-    });
+  for (const ChannelPart& part : parts)
+    for (int rank = 0; rank < n; rank++)
+      jobs.emplace_back([&, rank, part] {
+        runPatRank(channelComm(c, part.channel), &sh, rank, reduceScatter, sendbuffs[rank], recvbuffs[rank], count,
+                   esz, datatype, red, part);
+      });
   return runThreads(c, sh, jobs);
 }
 // The op stream of one rank, as plain ints for inspection: 12 per op, in the order of PatOp's fields
@@ -631,8 +644,11 @@ nexrResult_t patSchedule(bool reduceScatter, int nRanks, int rank, size_t count,
   const int64_t chunkCount = patChunkElems(&tmp, esz, !reduceScatter, (int64_t)count);
   if (chunkCount <= 0) return nexrInvalidArgument;
   const std::vector<PatOp> ops =
-      reduceScatter ? patOps(PatReduceScatterPlan((int)chunkCount, esz, (int64_t)count, rank, nRanks), parallelFactor)
-                    : patOps(PatAllGatherPlan((int)chunkCount, esz, (int64_t)count, rank, nRanks), parallelFactor);
+      reduceScatter
+          ? patOps(PatReduceScatterPlan((int)chunkCount, esz, 0, (int64_t)count, (int64_t)count, rank, nRanks),
+                   parallelFactor)
+          : patOps(PatAllGatherPlan((int)chunkCount, esz, 0, (int64_t)count, (int64_t)count, rank, nRanks),
+                   parallelFactor);
   *nOps = ops.size();
   if (out) {
     for (size_t i = 0; i < ops.size() && i < capOps; i++) {
@@ -665,7 +681,8 @@ nexrResult_t peerPat(nexrRingComm* c, bool reduceScatter, const void* sendbuff, 
   }
   Shared sh;
   sh.remoteAbort = &peerHeader(c->shm)->abort;
-  runPatRank(c, &sh, me, reduceScatter, sendbuff, recvbuff, count, esz, datatype, red);
+  const ChannelPart part{0, 0, (int64_t)count, patChunkElems(c, esz, !reduceScatter, (int64_t)count)};
+  runPatRank(c, &sh, me, reduceScatter, sendbuff, recvbuff, count, esz, datatype, red, part);
   return peerFinish(c, sh);
 }
 

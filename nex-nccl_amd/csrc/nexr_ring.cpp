@@ -102,20 +102,86 @@ int64_t chunkElems(const nexrRingComm* c, Geom g, size_t esz, bool tree, size_t 
   chunk = chunk / grain * grain;
   return chunk / (int64_t)esz;
 }
-// ---- schedules (one rank's view; 1 channel, userRanks[i] = (rank + i) % nranks) ----------------
+std::vector<ChannelPart> channelParts(const nexrRingComm* c, int64_t count, size_t esz, int trafficPerByteFn) {
+  const int64_t kMinTrafficPerChannel = 16 << 10;  // enqueue.cc:539
+  const int64_t nMaxChannels = c->cfg.nChannels > 0 ? c->cfg.nChannels : 1;
+  // Plan-level traffic split (:548-573) for this one task; the task may use every channel.
+  const int64_t taskTraffic = std::max<int64_t>(kMinTrafficPerChannel, count * (int64_t)esz * trafficPerByteFn);
+  const int64_t trafficPerChannel = std::max<int64_t>(kMinTrafficPerChannel, taskTraffic / nMaxChannels);
+  // Cell partition (:608-646).
+  int64_t channelId = 0;
+  const int64_t currentTraffic = 0;
+  const int64_t trafficPerByte = trafficPerByteFn * (c->proto == nexrRingProtoLL ? 4 : 1);
+  const int64_t cellSize = divUp(divUp(kMinTrafficPerChannel, trafficPerByte), 16) * 16;
+  const int64_t elementsPerCell = cellSize / (int64_t)esz;
+  const int64_t cells = divUp(count * (int64_t)esz, cellSize);
+  const int64_t trafficPerCell = cellSize * trafficPerByte;
+  int64_t cellsPerChannel = std::min(cells, divUp(trafficPerChannel, trafficPerCell));
+  int64_t cellsLo = channelId + 1 == nMaxChannels
+                        ? cells
+                        : std::min(cells, divUp(trafficPerChannel - currentTraffic, trafficPerCell));
+  int64_t nMidChannels = (cells - cellsLo) / cellsPerChannel;
+  int64_t cellsHi = (cells - cellsLo) % cellsPerChannel;
+  int64_t nChannels = (cellsLo != 0 ? 1 : 0) + nMidChannels + (cellsHi != 0 ? 1 : 0);
+  if (nMaxChannels < channelId + nChannels) {  // overflowed the available channels
+    nMidChannels = nMaxChannels - channelId - 2;
+    cellsPerChannel = (cells - cellsLo) / (nMidChannels + 1);
+    cellsHi = cellsPerChannel + (cells - cellsLo) % (nMidChannels + 1);
+  }
+  if (cellsHi == 0 && nMidChannels != 0) {
+    cellsHi = cellsPerChannel;
+    nMidChannels -= 1;
+  }
+  if (cellsLo == 0) {  // least channel skipped
+    channelId += 1;
+    if (nMidChannels == 0) {
+      cellsLo = cellsHi;
+      cellsHi = 0;
+    } else {
+      cellsLo = cellsPerChannel;
+      nMidChannels -= 1;
+    }
+  }
+  const int64_t countMid = nMidChannels != 0 ? cellsPerChannel * elementsPerCell : 0;
+  int64_t countLo = cellsLo * elementsPerCell;
+  int64_t countHi = cellsHi * elementsPerCell;
+  (countHi != 0 ? countHi : countLo) -= cells * elementsPerCell - count;
+  nChannels = (countLo != 0 ? 1 : 0) + nMidChannels + (cellsHi != 0 ? 1 : 0);
+  // ncclCollCbdPart (device.h:946-970) for channels channelLo .. channelLo + nChannels - 1.
+  std::vector<ChannelPart> parts;
+  const int64_t lo = channelId, hi = channelId + nChannels - 1;
+  for (int64_t ch = lo; ch <= hi; ch++) {
+    ChannelPart part{(int)ch, 0, 0, 0};
+    if (ch == lo) {
+      part.count = countLo;
+    } else if (ch == hi) {
+      part.offset = countLo + nMidChannels * countMid;
+      part.count = countHi;
+    } else {
+      part.offset = countLo + (ch - lo - 1) * countMid;
+      part.count = countMid;
+    }
+    parts.push_back(part);
+  }
+  return parts;
+}
+
+// ---- schedules (one rank's view of one channel, userRanks[i] = (rank + i) % nranks) -------------
+// Every schedule works on its channel's part of the data (ncclCollCbdPart, device.h:946-970):
+// elements [part.offset, part.offset + part.count) in chunks of part.chunkCount.
 
 // runRing for ncclAllReduce (all_reduce.h:12-84).
-void runRingAllReduce(Prims& p, int nranks, int64_t count) {
+void runRingAllReduce(Prims& p, int nranks, const ChannelPart& part) {
   const int ringIx = p.rank;
-  int64_t chunkCount = chunkElems(p.c, kGeomRing, p.esz, false, 0);
+  int64_t chunkCount = part.chunkCount;
   const int64_t loopCount = nranks * chunkCount;
   auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
-  for (int64_t elemOffset = 0; elemOffset < count; elemOffset += loopCount) {
-    const int64_t remCount = count - elemOffset;
+  for (int64_t elemOffset = 0; elemOffset < part.count; elemOffset += loopCount) {
+    const int64_t remCount = part.count - elemOffset;
     if (remCount < loopCount) chunkCount = alignUp(divUp(remCount, nranks), 16 / (int64_t)p.esz);
     auto at = [&](int chunk, int64_t* offset) {
       const int64_t chunkOffset = chunk * chunkCount;
-      *offset = elemOffset + chunkOffset;
+      *offset = part.offset + elemOffset + chunkOffset;
       return std::min(chunkCount, remCount - chunkOffset);
     };
     int64_t offset, nelem;
@@ -143,12 +209,11 @@ void runRingAllReduce(Prims& p, int nranks, int64_t count) {
 
 // runRing for ncclReduceScatter (reduce_scatter.h:12-52): `count` is the per-rank recvcount; the
 // segment of rankDest starts at rankDest*count in every sendbuff.
-void runRingReduceScatter(Prims& p, int nranks, int64_t count) {
-  const int64_t chunkCount = chunkElems(p.c, kGeomRing, p.esz, false, 0);
+void runRingReduceScatter(Prims& p, int nranks, int64_t count, const ChannelPart& part) {
   const int r = p.rank;
-  for (int64_t elemOffset = 0; elemOffset < count; elemOffset += chunkCount) {
-    const int64_t nelem = std::min(chunkCount, count - elemOffset);
-    const int64_t dataOffset = elemOffset;
+  for (int64_t elemOffset = 0; elemOffset < part.count; elemOffset += part.chunkCount) {
+    const int64_t nelem = std::min(part.chunkCount, part.count - elemOffset);
+    const int64_t dataOffset = part.offset + elemOffset;
     int rankDest = (r + nranks - 1) % nranks;  // ringRanks[nranks-1]
     if (!p.sendInput(dataOffset + rankDest * count, nelem)) return;
     for (int j = 2; j < nranks; ++j) {
@@ -161,12 +226,11 @@ void runRingReduceScatter(Prims& p, int nranks, int64_t count) {
 }
 
 // runRing for ncclAllGather (all_gather.h:12-66): `count` is the per-rank sendcount.
-void runRingAllGather(Prims& p, int nranks, int64_t count) {
-  const int64_t chunkCount = chunkElems(p.c, kGeomRing, p.esz, false, 0);
+void runRingAllGather(Prims& p, int nranks, int64_t count, const ChannelPart& part) {
   const int r = p.rank;
-  for (int64_t elemOffset = 0; elemOffset < count; elemOffset += chunkCount) {
-    const int64_t nelem = std::min(chunkCount, count - elemOffset);
-    const int64_t dataOffset = elemOffset;
+  for (int64_t elemOffset = 0; elemOffset < part.count; elemOffset += part.chunkCount) {
+    const int64_t nelem = std::min(part.chunkCount, part.count - elemOffset);
+    const int64_t dataOffset = part.offset + elemOffset;
     int64_t offset = dataOffset + (int64_t)r * count;
     // in place when the input chunk already sits at its place in the output (:52-56)
     const bool inPlace = p.userInput + dataOffset * p.esz == p.userOutput + offset * p.esz;
@@ -182,11 +246,11 @@ void runRingAllGather(Prims& p, int nranks, int64_t count) {
 }
 
 // runRing for ncclReduce (reduce.h:12-50).
-void runRingReduce(Prims& p, int nranks, int64_t count, int root) {
-  const int64_t chunkCount = chunkElems(p.c, kGeomPipe, p.esz, false, 0);
+void runRingReduce(Prims& p, int nranks, int root, const ChannelPart& part) {
   const int r = p.rank, prevRank = (r + nranks - 1) % nranks;
-  for (int64_t offset = 0; offset < count; offset += chunkCount) {
-    const int64_t nelem = std::min(chunkCount, count - offset);
+  for (int64_t elemOffset = 0; elemOffset < part.count; elemOffset += part.chunkCount) {
+    const int64_t offset = part.offset + elemOffset;
+    const int64_t nelem = std::min(part.chunkCount, part.count - elemOffset);
     bool ok;
     if (prevRank == root) ok = p.sendInput(offset, nelem);
     else if (r == root) ok = p.recvReduceCopy(offset, offset, nelem, /*postOp=*/true);
@@ -196,11 +260,11 @@ void runRingReduce(Prims& p, int nranks, int64_t count, int root) {
 }
 
 // runRing for ncclBroadcast (broadcast.h:12-58).
-void runRingBroadcast(Prims& p, int nranks, int64_t count, int root) {
-  const int64_t chunkCount = chunkElems(p.c, kGeomPipe, p.esz, false, 0);
+void runRingBroadcast(Prims& p, int nranks, int root, const ChannelPart& part) {
   const int r = p.rank, nextRank = (r + 1) % nranks;
-  for (int64_t offset = 0; offset < count; offset += chunkCount) {
-    const int64_t nelem = std::min(chunkCount, count - offset);
+  for (int64_t elemOffset = 0; elemOffset < part.count; elemOffset += part.chunkCount) {
+    const int64_t offset = part.offset + elemOffset;
+    const int64_t nelem = std::min(part.chunkCount, part.count - elemOffset);
     bool ok;
     if (r == root) ok = p.userInput == p.userOutput ? p.sendInput(offset, nelem) : p.copySend(offset, offset, nelem);
     else if (nextRank == root) ok = p.recvOutput(offset, nelem);
@@ -214,10 +278,10 @@ void runRingBroadcast(Prims& p, int nranks, int64_t count, int root) {
 // other rank runs a reduce-up half (FanAsymmetric<3,1>) and a broadcast-down half
 // (FanAsymmetric<1,3>) side by side.
 enum TreeRole { kTreeRoot, kTreeReduceUp, kTreeBcastDown };
-void runTree(Prims& p, int64_t count, TreeRole role, bool leaf) {
-  const int64_t chunkCount = chunkElems(p.c, kGeomPipe, p.esz, true, (size_t)count * p.esz);
-  for (int64_t offset = 0; offset < count; offset += chunkCount) {
-    const int64_t nelem = std::min(chunkCount, count - offset);
+void runTree(Prims& p, TreeRole role, bool leaf, const ChannelPart& part) {
+  for (int64_t elemOffset = 0; elemOffset < part.count; elemOffset += part.chunkCount) {
+    const int64_t offset = part.offset + elemOffset;
+    const int64_t nelem = std::min(part.chunkCount, part.count - elemOffset);
     bool ok;
     if (role == kTreeRoot) ok = p.recvReduceCopySend(offset, offset, nelem, /*postOp=*/true);
     else if (role == kTreeReduceUp) ok = leaf ? p.sendInput(offset, nelem) : p.recvReduceSend(offset, nelem);
@@ -456,24 +520,30 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
   }
   if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
   const Geom g = (coll == kReduce || coll == kBroadcast) ? kGeomPipe : kGeomRing;
+  const int trafficPerByte = coll == kAllReduce ? 2 : (coll == kReduceScatter || coll == kAllGather) ? n : 1;
+  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, trafficPerByte);
+  for (ChannelPart& part : parts) part.chunkCount = chunkElems(channelComm(c, part.channel), g, esz, false, 0);
   Shared sh;
   std::vector<std::function<void()>> jobs;
-  for (int rank = 0; rank < n; rank++) {
-    jobs.emplace_back([&, rank] {
-      if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-      Prims p = makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, g, c->streams[rank],
-                          c->status[rank]);
-      p.recv[p.nRecv++] = c->conns[rank];
-      p.send[p.nSend++] = c->conns[(rank + 1) % n];
-      p.attach();
-      switch (coll) {
-        case kAllReduce: runRingAllReduce(p, n, (int64_t)count); break;
-        case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count); break;
-        case kAllGather: runRingAllGather(p, n, (int64_t)count); break;
-        case kReduce: runRingReduce(p, n, (int64_t)count, root); break;
-        case kBroadcast: runRingBroadcast(p, n, (int64_t)count, root); break;
-      }
-    });
+  for (const ChannelPart& part : parts) {
+    for (int rank = 0; rank < n; rank++) {
+      jobs.emplace_back([&, rank, part] {
+        nexrRingComm* ck = channelComm(c, part.channel);
+        if (ck->streams[rank]) (void)hipSetDevice(ck->devices[rank]);
+        Prims p = makePrims(ck, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, g,
+                            ck->streams[rank], ck->status[rank]);
+        p.recv[p.nRecv++] = ck->conns[rank];
+        p.send[p.nSend++] = ck->conns[(rank + 1) % n];
+        p.attach();
+        switch (coll) {
+          case kAllReduce: runRingAllReduce(p, n, part); break;
+          case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count, part); break;
+          case kAllGather: runRingAllGather(p, n, (int64_t)count, part); break;
+          case kReduce: runRingReduce(p, n, root, part); break;
+          case kBroadcast: runRingBroadcast(p, n, root, part); break;
+        }
+      });
+    }
   }
   return runThreads(c, sh, jobs);
 }
@@ -501,12 +571,13 @@ nexrResult_t peerCollective(nexrRingComm* c, RingColl coll, const void* sendbuff
   p.recv[p.nRecv++] = c->conns[me];
   p.send[p.nSend++] = c->conns[(me + 1) % n];
   p.attach();
+  const ChannelPart part{0, 0, (int64_t)count, chunkElems(c, g, esz, false, 0)};  // process ranks: 1 channel
   switch (coll) {
-    case kAllReduce: runRingAllReduce(p, n, (int64_t)count); break;
-    case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count); break;
-    case kAllGather: runRingAllGather(p, n, (int64_t)count); break;
-    case kReduce: runRingReduce(p, n, (int64_t)count, root); break;
-    case kBroadcast: runRingBroadcast(p, n, (int64_t)count, root); break;
+    case kAllReduce: runRingAllReduce(p, n, part); break;
+    case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count, part); break;
+    case kAllGather: runRingAllGather(p, n, (int64_t)count, part); break;
+    case kReduce: runRingReduce(p, n, root, part); break;
+    case kBroadcast: runRingBroadcast(p, n, root, part); break;
   }
   if (sh.firstError.load() != 0) {
     c->broken = true;
@@ -614,6 +685,7 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   if (cfg->treeRanksPerNode < 0 || (cfg->treeRanksPerNode > 0 && cfg->nRanks % cfg->treeRanksPerNode != 0) ||
       (cfg->treeIndex != 0 && cfg->treeIndex != 1))
     return nexrInvalidArgument;
+  if (cfg->nChannels < 0 || cfg->nChannels > kMaxChannels) return nexrInvalidArgument;
   // The LL/LL128 kernels poll live FIFO lines: they need device-visible lines, i.e. device memory,
   // unless the caller supplies its own step implementation (e.g. a CPU checker).
   if (cfg->memMode == nexrRingHostMemory && ((cfg->protocol == nexrRingProtoLL && !cfg->llFn) ||
@@ -676,6 +748,22 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
       }
     }
   }
+  // Channels 1..nChannels-1: the same communicator again. The reference duplicates its channels and
+  // gives the copies the other tree of the double binary tree (graph/connect.cc:146-160).
+  const int nCh = cfg->nChannels > 0 ? cfg->nChannels : 1;
+  c->cfg.nChannels = nCh;
+  for (int k = 1; k < nCh; k++) {
+    nexrRingConfig sub = *cfg;
+    sub.nChannels = 1;
+    sub.treeIndex = (cfg->treeIndex + (nCh >= 2 && k >= nCh / 2 ? 1 : 0)) % 2;
+    nexrRingComm_t sc = nullptr;
+    nexrResult_t res = nexrRingCommCreate(&sc, &sub);
+    if (res != nexrSuccess) {
+      nexrRingCommDestroy(c);
+      return res;
+    }
+    c->channels.push_back(sc);
+  }
   *out = c;
   return nexrSuccess;
 }
@@ -718,51 +806,60 @@ NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sen
   for (int i = 0; i < n; i++)
     if (!sendbuffs[i] || !recvbuffs[i]) return nexrInvalidArgument;
   if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
-  r = ensureTree(c);
-  if (r != nexrSuccess) {
-    c->broken = true;
-    return r;
+  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, /*ncclFuncAllReduce*/ 2);
+  for (ChannelPart& part : parts) {
+    nexrRingComm* ck = channelComm(c, part.channel);
+    r = ensureTree(ck);
+    if (r != nexrSuccess) {
+      c->broken = true;
+      return r;
+    }
+    // calcCollChunking for the part: nBytes = its count x esz (enqueue.cc:664-679)
+    part.chunkCount = chunkElems(ck, kGeomPipe, esz, true, (size_t)part.count * esz);
   }
   Shared sh;
   std::vector<std::function<void()>> jobs;
-  for (int rank = 0; rank < n; rank++) {
-    const TreeLinks& t = c->tree[rank];
-    const bool leaf = t.down[0] == -1;
-    auto make = [&, rank](hipStream_t s, uint32_t* st) {
-      return makePrims(c, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, kGeomPipe, s, st);
-    };
-    if (t.up == -1) {  // root: recv from and send to every child
-      jobs.emplace_back([&, rank, make] {
-        if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-        Prims p = make(c->streams[rank], c->status[rank]);
-        const TreeLinks& tl = c->tree[rank];
-        for (int i = 0; i < tl.nDown(); i++) {
-          p.recv[p.nRecv++] = c->treeUp[tl.down[i]];
-          p.send[p.nSend++] = c->treeDown[tl.down[i]];
-        }
+  for (const ChannelPart& part : parts) {
+    nexrRingComm* ck = channelComm(c, part.channel);
+    for (int rank = 0; rank < n; rank++) {
+      const TreeLinks& t = ck->tree[rank];
+      const bool leaf = t.down[0] == -1;
+      auto make = [&, rank, ck](hipStream_t s, uint32_t* st) {
+        return makePrims(ck, &sh, rank, sendbuffs[rank], recvbuffs[rank], esz, datatype, red, kGeomPipe, s, st);
+      };
+      if (t.up == -1) {  // root: recv from and send to every child
+        jobs.emplace_back([&, rank, make, ck, part] {
+          if (ck->streams[rank]) (void)hipSetDevice(ck->devices[rank]);
+          Prims p = make(ck->streams[rank], ck->status[rank]);
+          const TreeLinks& tl = ck->tree[rank];
+          for (int i = 0; i < tl.nDown(); i++) {
+            p.recv[p.nRecv++] = ck->treeUp[tl.down[i]];
+            p.send[p.nSend++] = ck->treeDown[tl.down[i]];
+          }
+          p.attach();
+          runTree(p, kTreeRoot, false, part);
+        });
+        continue;
+      }
+      jobs.emplace_back([&, rank, leaf, make, ck, part] {  // reduce up: recv from children, send to the parent
+        if (ck->streams[rank]) (void)hipSetDevice(ck->devices[rank]);
+        Prims p = make(ck->streams[rank], ck->status[rank]);
+        const TreeLinks& tl = ck->tree[rank];
+        for (int i = 0; i < tl.nDown(); i++) p.recv[p.nRecv++] = ck->treeUp[tl.down[i]];
+        p.send[p.nSend++] = ck->treeUp[rank];
         p.attach();
-        runTree(p, (int64_t)count, kTreeRoot, false);
+        runTree(p, kTreeReduceUp, leaf, part);
       });
-      continue;
+      jobs.emplace_back([&, rank, leaf, make, ck, part] {  // broadcast down: recv from the parent, send to children
+        if (ck->streams2[rank]) (void)hipSetDevice(ck->devices[rank]);
+        Prims p = make(ck->streams2[rank], ck->status2[rank]);
+        const TreeLinks& tl = ck->tree[rank];
+        p.recv[p.nRecv++] = ck->treeDown[rank];
+        for (int i = 0; i < tl.nDown(); i++) p.send[p.nSend++] = ck->treeDown[tl.down[i]];
+        p.attach();
+        runTree(p, kTreeBcastDown, leaf, part);
+      });
     }
-    jobs.emplace_back([&, rank, leaf, make] {  // reduce up: recv from children, send to the parent
-      if (c->streams[rank]) (void)hipSetDevice(c->devices[rank]);
-      Prims p = make(c->streams[rank], c->status[rank]);
-      const TreeLinks& tl = c->tree[rank];
-      for (int i = 0; i < tl.nDown(); i++) p.recv[p.nRecv++] = c->treeUp[tl.down[i]];
-      p.send[p.nSend++] = c->treeUp[rank];
-      p.attach();
-      runTree(p, (int64_t)count, kTreeReduceUp, leaf);
-    });
-    jobs.emplace_back([&, rank, leaf, make] {  // broadcast down: recv from the parent, send to children
-      if (c->streams2[rank]) (void)hipSetDevice(c->devices[rank]);
-      Prims p = make(c->streams2[rank], c->status2[rank]);
-      const TreeLinks& tl = c->tree[rank];
-      p.recv[p.nRecv++] = c->treeDown[rank];
-      for (int i = 0; i < tl.nDown(); i++) p.send[p.nSend++] = c->treeDown[tl.down[i]];
-      p.attach();
-      runTree(p, (int64_t)count, kTreeBcastDown, leaf);
-    });
   }
   return runThreads(c, sh, jobs);
 }
@@ -776,6 +873,8 @@ NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t c, int rank, int* up, int*
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
   if (!c) return nexrInvalidArgument;
+  for (nexrRingComm* ch : c->channels) nexrRingCommDestroy(ch);
+  c->channels.clear();
   if (c->peer) {
     if (!c->streams.empty() && c->streams[c->self]) (void)hipStreamSynchronize(c->streams[c->self]);
     const int next = (c->self + 1) % c->cfg.nRanks;

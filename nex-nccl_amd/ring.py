@@ -38,7 +38,7 @@ class RingConfig(ctypes.Structure):
     _fields_ = [("nRanks", ctypes.c_int), ("buffBytes", ctypes.c_size_t), ("memMode", ctypes.c_int),
                 ("fn", ctypes.c_void_p), ("timeoutMs", ctypes.c_int), ("protocol", ctypes.c_int),
                 ("llFn", ctypes.c_void_p), ("ll128Fn", ctypes.c_void_p), ("treeRanksPerNode", ctypes.c_int),
-                ("treeIndex", ctypes.c_int)]
+                ("treeIndex", ctypes.c_int), ("nChannels", ctypes.c_int)]
 
 
 class PeerRingConfig(ctypes.Structure):
@@ -122,9 +122,9 @@ class RingComm:
     def __init__(self, n_ranks: int, mem_mode: int = HOST_MEMORY, buff_bytes: int = 0,
                  fn_address: Optional[int] = None, timeout_ms: int = 0, protocol: int = PROTO_SIMPLE,
                  ll_fn_address: Optional[int] = None, ll128_fn_address: Optional[int] = None,
-                 tree_ranks_per_node: int = 0, tree_index: int = 0):
+                 tree_ranks_per_node: int = 0, tree_index: int = 0, n_channels: int = 0):
         cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms, protocol,
-                         ll_fn_address or None, ll128_fn_address or None, tree_ranks_per_node, tree_index)
+                         ll_fn_address or None, ll128_fn_address or None, tree_ranks_per_node, tree_index, n_channels)
         h = ctypes.c_void_p()
         _check(ring_lib().nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
         self._h = h

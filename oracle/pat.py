@@ -67,11 +67,12 @@ def _step():
 
 
 class RsPlan(_Geometry):
-    """PatRSAlgorithm (collectives.h:434-684)."""
+    """PatRSAlgorithm (collectives.h:434-684) over the channel part [offset, end) of `count`."""
 
-    def __init__(self, chunk, esz, count, rank, nranks):
-        super().__init__(chunk * esz, NCCL_STEPS, MAX_PARALLEL, count, esz, nranks)
-        self.offset, self.end, self.count, self.chunk = 0, count, count, chunk
+    def __init__(self, chunk, esz, count, rank, nranks, offset=0, end=None):
+        end = count if end is None else end
+        super().__init__(chunk * esz, NCCL_STEPS, MAX_PARALLEL, end - offset, esz, nranks)
+        self.offset, self.end, self.count, self.chunk = offset, end, count, chunk
         self.rank, self.n = rank, nranks
         self._reset()
 
@@ -213,11 +214,12 @@ class RsPlan(_Geometry):
 
 
 class AgPlan(_Geometry):
-    """PatAGAlgorithm (collectives.h:687-906)."""
+    """PatAGAlgorithm (collectives.h:687-906) over the channel part [offset, end) of `count`."""
 
-    def __init__(self, chunk, esz, count, rank, nranks):
-        super().__init__(chunk * esz, NCCL_STEPS, MAX_PARALLEL, count, esz, nranks)
-        self.offset, self.end, self.count, self.chunk = 0, count, count, chunk
+    def __init__(self, chunk, esz, count, rank, nranks, offset=0, end=None):
+        end = count if end is None else end
+        super().__init__(chunk * esz, NCCL_STEPS, MAX_PARALLEL, end - offset, esz, nranks)
+        self.offset, self.end, self.count, self.chunk = offset, end, count, chunk
         self.rank, self.n = rank, nranks
         self.as_dim = _log2_up(self.agg_delta)
         self._reset()
@@ -331,10 +333,11 @@ class AgPlan(_Geometry):
         return ps
 
 
-def schedule(reduce_scatter, n_ranks, rank, count, esz, step_bytes):
-    """Every ncclPatStep of one rank's compute thread, and parallelFactor."""
-    chunk = chunk_count(n_ranks, count, esz, step_bytes, not reduce_scatter)
-    plan = (RsPlan if reduce_scatter else AgPlan)(chunk, esz, count, rank, n_ranks)
+def schedule(reduce_scatter, n_ranks, rank, count, esz, step_bytes, offset=0, end=None):
+    """Every ncclPatStep of one rank's compute thread for the part [offset, end), and parallelFactor."""
+    end = count if end is None else end
+    chunk = chunk_count(n_ranks, end - offset, esz, step_bytes, not reduce_scatter)
+    plan = (RsPlan if reduce_scatter else AgPlan)(chunk, esz, count, rank, n_ranks, offset, end)
     ops = []
     while True:
         ops.append(plan.next())
@@ -342,7 +345,16 @@ def schedule(reduce_scatter, n_ranks, rank, count, esz, step_bytes):
             return ops, plan.parallel_factor
 
 
-def _simulate(reduce_scatter, inputs, outputs, esz, step_bytes, fold):
+def _simulate(reduce_scatter, inputs, outputs, esz, step_bytes, fold, n_channels=1):
+    """Runs every channel's part: each channel has its own links (fresh FIFOs and counters)."""
+    n = len(inputs)
+    count = outputs[0].size // (1 if reduce_scatter else n)
+    from .ring import channel_parts
+    for _, lo, cnt in channel_parts(n_channels, count, esz, n):
+        _simulate_part(reduce_scatter, inputs, outputs, esz, step_bytes, fold, lo, lo + cnt)
+
+
+def _simulate_part(reduce_scatter, inputs, outputs, esz, step_bytes, fold, offset, end):
     """Runs every rank's batches; `fold(srcs, dsts)` performs one reduceCopy on numpy views."""
     n = len(inputs)
     count = outputs[0].size // (1 if reduce_scatter else n)
@@ -352,7 +364,7 @@ def _simulate(reduce_scatter, inputs, outputs, esz, step_bytes, fold):
     tail = {}   # (from, to) -> steps published by the sender
     state = []
     for r in range(n):
-        ops, pf = schedule(reduce_scatter, n, r, count, esz, step_bytes)
+        ops, pf = schedule(reduce_scatter, n, r, count, esz, step_bytes, offset, end)
         dims = [d for d in range(32) if (1 << d) < n]
         lo = {d: (r - (1 << d)) % n for d in dims}
         hi = {d: (r + (1 << d)) % n for d in dims}
@@ -465,7 +477,7 @@ def _simulate(reduce_scatter, inputs, outputs, esz, step_bytes, fold):
             raise RuntimeError("PAT schedule deadlocked")
 
 
-def reduce_scatter_expected(inputs, datatype, dev_op, arg, step_bytes=(4 << 20) // NCCL_STEPS):
+def reduce_scatter_expected(inputs, datatype, dev_op, arg, step_bytes=(4 << 20) // NCCL_STEPS, n_channels=1):
     """Every rank's output of the PAT ncclReduceScatter (recvcount = input size / nRanks)."""
     n = len(inputs)
     esz = inputs[0].itemsize
@@ -477,11 +489,11 @@ def reduce_scatter_expected(inputs, datatype, dev_op, arg, step_bytes=(4 << 20) 
         res = reduce_copy([np.array(s) for s in srcs], 1, datatype, dev_op, arg)[0]
         dsts[0][...] = res
 
-    _simulate(True, inputs, outputs, esz, step_bytes, fold)
+    _simulate(True, inputs, outputs, esz, step_bytes, fold, n_channels)
     return outputs
 
 
-def all_gather_expected(inputs, step_bytes=(4 << 20) // NCCL_STEPS, outputs=None):
+def all_gather_expected(inputs, step_bytes=(4 << 20) // NCCL_STEPS, outputs=None, n_channels=1):
     """Every rank's output of the PAT ncclAllGather (inputs in place when `outputs` holds them)."""
     n = len(inputs)
     count = inputs[0].size
@@ -492,5 +504,5 @@ def all_gather_expected(inputs, step_bytes=(4 << 20) // NCCL_STEPS, outputs=None
         for d in dsts:
             d[...] = srcs[0]
 
-    _simulate(False, inputs, outputs, inputs[0].itemsize, step_bytes, fold)
+    _simulate(False, inputs, outputs, inputs[0].itemsize, step_bytes, fold, n_channels)
     return outputs

@@ -25,7 +25,57 @@ def _align_up(a: int, b: int) -> int:
     return _div_up(a, b) * b
 
 
-def ring_allreduce_expected(inputs, datatype: int, op: int, buff_bytes: int = 4 << 20):
+def channel_parts(n_channels: int, count: int, esz: int, traffic_per_byte: int, ll: bool = False):
+    """[(channel, offset, count)] of one collective split over `n_channels` channels: the planner's
+    cell partition for a task alone in its plan (reference src/enqueue.cc:539-690; trafficPerByte
+    of :74-81, x4 for LL) and ncclCollCbdPart's per-channel view (src/include/device.h:946-970)."""
+    min_traffic = 16 << 10
+    n_max = max(1, n_channels)
+    task_traffic = max(min_traffic, count * esz * traffic_per_byte)
+    per_channel = max(min_traffic, task_traffic // n_max)
+    tpb = traffic_per_byte * (4 if ll else 1)
+    cell = _div_up(_div_up(min_traffic, tpb), 16) * 16
+    per_cell_elems = cell // esz
+    cells = _div_up(count * esz, cell)
+    cell_traffic = cell * tpb
+    ch0 = 0
+    cells_per_ch = min(cells, _div_up(per_channel, cell_traffic))
+    lo_cells = cells if ch0 + 1 == n_max else min(cells, _div_up(per_channel, cell_traffic))
+    n_mid = (cells - lo_cells) // cells_per_ch
+    hi_cells = (cells - lo_cells) % cells_per_ch
+    used = (1 if lo_cells else 0) + n_mid + (1 if hi_cells else 0)
+    if n_max < ch0 + used:
+        n_mid = n_max - ch0 - 2
+        cells_per_ch = (cells - lo_cells) // (n_mid + 1)
+        hi_cells = cells_per_ch + (cells - lo_cells) % (n_mid + 1)
+    if hi_cells == 0 and n_mid != 0:
+        hi_cells, n_mid = cells_per_ch, n_mid - 1
+    if lo_cells == 0:
+        ch0 += 1
+        if n_mid == 0:
+            lo_cells, hi_cells = hi_cells, 0
+        else:
+            lo_cells, n_mid = cells_per_ch, n_mid - 1
+    mid_count = cells_per_ch * per_cell_elems if n_mid else 0
+    lo_count, hi_count = lo_cells * per_cell_elems, hi_cells * per_cell_elems
+    excess = cells * per_cell_elems - count
+    if hi_count:
+        hi_count -= excess
+    else:
+        lo_count -= excess
+    used = (1 if lo_count else 0) + n_mid + (1 if hi_cells else 0)
+    parts = []
+    for k in range(used):
+        if k == 0:
+            parts.append((ch0, 0, lo_count))
+        elif k == used - 1:
+            parts.append((ch0 + k, lo_count + n_mid * mid_count, hi_count))
+        else:
+            parts.append((ch0 + k, lo_count + (k - 1) * mid_count, mid_count))
+    return parts
+
+
+def ring_allreduce_expected(inputs, datatype: int, op: int, buff_bytes: int = 4 << 20, n_channels: int = 1):
     n = len(inputs)
     enc = host_to_dev_red_op(op, datatype, n)
     if enc is None:
@@ -43,31 +93,32 @@ def ring_allreduce_expected(inputs, datatype: int, op: int, buff_bytes: int = 4 
             out = inputs[0].copy()
         return [out]
     step_bytes = buff_bytes // 8
-    chunk = step_bytes * 4 // 512 * 512 // esz  # chunkSize aligned to the 512-B grain (enqueue.cc:2062)
-    loop = n * chunk
-    for elem_off in range(0, count, loop):
-        rem = count - elem_off
-        if rem < loop:
-            chunk = _align_up(_div_up(rem, n), 16 // esz)
-        for c in range(n):
-            lo = elem_off + c * chunk
-            hi = min(elem_off + c * chunk + chunk, count)
-            if hi <= lo:
-                continue
-            sl = slice(lo, hi)
-            r = (c + 1) % n
-            # directSend: K=1 with the pre-op on the local input
-            acc = reduce_copy([inputs[r][sl]], 1, datatype, dev_op, arg, [arg], False)[0]
-            for k in range(2, n + 1):
-                r = (c + k) % n
-                post = k == n  # directRecvReduceCopyDirectSend(postOp=true) at rank c
-                acc = reduce_copy([inputs[r][sl], acc], 1, datatype, dev_op, arg, [arg], post)[0]
-            out[sl] = acc
+    for _, grid, part_count in channel_parts(n_channels, count, esz, 2):
+        chunk = step_bytes * 4 // 512 * 512 // esz  # chunkSize aligned to the 512-B grain (enqueue.cc:2062)
+        loop = n * chunk
+        for elem_off in range(0, part_count, loop):
+            rem = part_count - elem_off
+            if rem < loop:
+                chunk = _align_up(_div_up(rem, n), 16 // esz)
+            for c in range(n):
+                lo = grid + elem_off + c * chunk
+                hi = grid + min(elem_off + c * chunk + chunk, part_count)
+                if hi <= lo:
+                    continue
+                sl = slice(lo, hi)
+                r = (c + 1) % n
+                # directSend: K=1 with the pre-op on the local input
+                acc = reduce_copy([inputs[r][sl]], 1, datatype, dev_op, arg, [arg], False)[0]
+                for k in range(2, n + 1):
+                    r = (c + k) % n
+                    post = k == n  # directRecvReduceCopyDirectSend(postOp=true) at rank c
+                    acc = reduce_copy([inputs[r][sl], acc], 1, datatype, dev_op, arg, [arg], post)[0]
+                out[sl] = acc
     return [out.copy() for _ in range(n)]
 
 
 def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int = 8 * 512 * 8 * 16,
-                               proto: str = "ll"):
+                               proto: str = "ll", n_channels: int = 1):
     """The LL / LL128-protocol ring: same runRing schedule (chunk = stepBytes/2 for LL,
     stepBytes/16*15 on the 1920-B grain for LL128, src/enqueue.cc:1997-1999), but every step folds
     with the received PEER partial as the first operand (prims_ll.h:251-258, prims_ll128.h:214-219)."""
@@ -83,6 +134,13 @@ def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int =
     if count == 0 or n == 1:
         return ring_allreduce_expected(inputs, datatype, op)
     out = np.empty_like(inputs[0])
+    for _, grid, part_count in channel_parts(n_channels, count, esz, 2, ll=proto == "ll"):
+        _ll_ring_part(step, inputs, out, grid, part_count, esz, buff_bytes, proto, datatype, dev_op, arg)
+    return [out.copy() for _ in range(n)]
+
+
+def _ll_ring_part(step, inputs, out, grid, count, esz, buff_bytes, proto, datatype, dev_op, arg):
+    n = len(inputs)
     if proto == "ll":
         chunk = (buff_bytes // 8) // 2 // 16 * 16 // esz
     else:
@@ -93,8 +151,8 @@ def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int =
         if rem < loop:
             chunk = _align_up(_div_up(rem, n), 16 // esz)
         for c in range(n):
-            lo = elem_off + c * chunk
-            hi = min(lo + chunk, count)
+            lo = grid + elem_off + c * chunk
+            hi = grid + min(elem_off + c * chunk + chunk, count)
             if hi <= lo:
                 continue
             m = hi - lo
@@ -107,7 +165,6 @@ def ring_allreduce_expected_ll(inputs, datatype: int, op: int, buff_bytes: int =
                                       post)
                 assert rc == 0
             out[lo:hi] = dst.view(out.dtype)
-    return [out.copy() for _ in range(n)]
 
 
 # ---- the other collectives that reach reduceCopy through genericOp --------------------------------
@@ -239,6 +296,21 @@ def tree_topology(n_ranks: int, ranks_per_node: int = 0, tree_index: int = 0):
             down += [d * L for d in (d0, d1) if d != -1]
         links.append((up, down))
     return links
+
+
+def tree_allreduce_expected_channels(inputs, datatype: int, op: int, links_of, n_channels: int,
+                                     proto: str = "simple"):
+    """The tree all-reduce split over channels: each channel folds its part over its own tree,
+    `links_of(channel)` (the upper half of 2+ channels runs the other tree of the double binary tree,
+    graph/connect.cc:146-160)."""
+    n = len(inputs)
+    if n == 1 or inputs[0].size == 0:
+        return tree_allreduce_expected(inputs, datatype, op, links_of(0), proto)
+    out = np.empty_like(inputs[0])
+    for ch, grid, cnt in channel_parts(n_channels, inputs[0].size, inputs[0].itemsize, 2, ll=proto == "ll"):
+        sl = slice(grid, grid + cnt)
+        out[sl] = tree_allreduce_expected([x[sl] for x in inputs], datatype, op, links_of(ch), proto)[0]
+    return [out.copy() for _ in range(n)]
 
 
 def tree_allreduce_expected(inputs, datatype: int, op: int, links, proto: str = "simple"):

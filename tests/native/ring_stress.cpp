@@ -40,6 +40,7 @@ int main() {
       cfg.timeoutMs = 60000;
       cfg.protocol = protos[pi];
       cfg.treeRanksPerNode = n == 4 ? 2 : 1;  // 4 ranks: 2 nodes of 2 (arity-3 heads); else a btree
+      cfg.nChannels = n == 4 ? 3 : 2;          // concurrent channels (their own threads and links)
       nexrRingComm_t comm;
       if (nexrRingCommCreate(&comm, &cfg) != nexrSuccess) { printf("create failed\n"); return 2; }
       for (int iter = 0; iter < 3; iter++) {

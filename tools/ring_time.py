@@ -45,7 +45,8 @@ def run(n, mode_name, proto_name, coll, iters):
         send, recv = x, [np.zeros(out_n, np.float32) for _ in range(n)]
         sp, rp = [v.ctypes.data for v in send], [v.ctypes.data for v in recv]
     fns = ORACLE_FNS if mode_name == "cpu-oracle" else (None, None, None)
-    kw = dict(protocol=proto, ll_fn_address=fns[1], ll128_fn_address=fns[2], tree_ranks_per_node=1)
+    kw = dict(protocol=proto, ll_fn_address=fns[1], ll128_fn_address=fns[2], tree_ranks_per_node=1,
+              n_channels=int(os.environ.get("RING_TIME_CHANNELS", "1")))
     with ring.RingComm(n, mode, 0, fns[0], **kw) as comm:
         call = {"allreduce": lambda: comm.all_reduce(sp, rp, count, F32, 0),
                 "tree": lambda: comm.tree_all_reduce(sp, rp, count, F32, 0),
