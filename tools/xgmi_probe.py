@@ -7,9 +7,13 @@ enabled both ways, and the reduce-copy kernel run on GPU 0 with one operand in G
   remote write srcs = [a0, b0] -> d1          (the NCCL_P2P_WRITE pattern: the result lands in the
                                                 next GPU's memory, src/transport/p2p.cc:402)
 
-fp32 sum, 256 MiB per buffer. Prints one JSON line; with fewer than two GPUs it prints a "skipped"
-line and exits 0. bench.py runs it as a bounded subprocess when it drives more than one GPU, so a
-failure here can never take the bench line down with it.
+fp32 sum, 256 MiB per buffer. Then the process-rank ring itself across the two GPUs
+(`ring_processes`): two child processes, rank r on GPU r, each mapping the other's FIFO over IPC
+(nexrPeerRingCommCreate), run the emulated ring all-reduce (C1's 4 MiB and 64 MiB of fp32 per rank,
+SIMPLE) with every step's reduce-copy writing into the peer GPU's HBM over xGMI; results are checked
+exactly (integer-valued inputs). Prints one JSON line; with fewer than two GPUs it prints a
+"skipped" line and exits 0. bench.py runs it as a bounded subprocess when it drives more than one
+GPU, so a failure here can never take the bench line down with it.
 """
 import ctypes
 import importlib
@@ -81,9 +85,73 @@ def main() -> int:
     ok_write = torch.equal(o1.to(d0), a0 + b0)
     out["remote_write"] = {"us": round(t * 1e6, 1), "xgmi_GBps": round(buf / t / 1e9, 1),
                            "alg_GBps": round(3 * buf / t / 1e9, 1), "exact": bool(ok_write)}
+    out["ring_processes"] = ring_processes()
     print(json.dumps(out), flush=True)
     return 0
 
 
+def ring_rank(rank: int, shm: str, counts) -> int:
+    """One rank of the cross-GPU process ring (child process, GPU `rank`)."""
+    import time
+    import numpy as np
+    import torch
+    dev = rank % torch.cuda.device_count()  # GPU r; both on GPU 0 when rehearsing on a one-GPU box
+    torch.cuda.set_device(dev)
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    res = {}
+    with ring.PeerRingComm(2, rank, shm, device=dev, timeout_ms=30000) as comm:
+        for count in counts:
+            x = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) + rank
+            y = torch.empty_like(x)
+            exp = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) * 2 + 1
+            torch.cuda.synchronize()
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)  # warm-up, connects the FIFOs
+            iters = 5
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)
+            dt = (time.perf_counter() - t0) / iters
+            res[str(count * 4)] = {"ms": round(dt * 1e3, 3), "algbw_GBps": round(count * 4 / dt / 1e9, 2),
+                                   "exact": bool(torch.equal(y, exp))}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    del np
+    return 0
+
+
+def ring_processes(timeout_s: float = 60.0):
+    import subprocess
+    import uuid
+    shm = f"/nexr_xgmi_{uuid.uuid4().hex[:12]}"
+    counts = "1048576,16777216"
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--ring-rank", str(r), "--shm", shm,
+                               "--counts", counts], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              start_new_session=True) for r in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=timeout_s))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, 9)
+                p.wait()
+        return {"error": "timeout"}
+    finally:
+        if os.path.exists("/dev/shm" + shm):
+            os.unlink("/dev/shm" + shm)
+    if any(p.returncode != 0 for p in procs):
+        return {"error": [p.returncode for p in procs], "stderr": [e[-300:] for _, e in outs]}
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    return {"per_rank_bytes": json.loads(lines[-1]), "ranks": "2 processes, rank r on GPU r, SIMPLE, fp32 sum"}
+
+
 if __name__ == "__main__":
+    if "--ring-only" in sys.argv:  # rehearsal of the process ring alone (any number of GPUs)
+        print(json.dumps(ring_processes()), flush=True)
+        sys.exit(0)
+    if "--ring-rank" in sys.argv:
+        a = sys.argv
+        sys.exit(ring_rank(int(a[a.index("--ring-rank") + 1]), a[a.index("--shm") + 1],
+                           [int(v) for v in a[a.index("--counts") + 1].split(",")]))
     sys.exit(main())
