@@ -283,7 +283,7 @@ def main(argv=None):
     return result
 
 
-def xgmi_probe(timeout_s: float = 90.0):
+def xgmi_probe(timeout_s: float = 150.0):
     """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, in a bounded
     subprocess: its outcome is reported, never allowed to fail the bench line."""
     import subprocess

@@ -119,7 +119,7 @@ def ring_rank(rank: int, shm: str, counts) -> int:
     return 0
 
 
-def ring_processes(timeout_s: float = 60.0):
+def ring_processes(timeout_s: float = 45.0):
     import subprocess
     import uuid
     shm = f"/nexr_xgmi_{uuid.uuid4().hex[:12]}"
