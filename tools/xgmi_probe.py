@@ -93,7 +93,6 @@ def main() -> int:
 def ring_rank(rank: int, shm: str, counts) -> int:
     """One rank of the cross-GPU process ring (child process, GPU `rank`)."""
     import time
-    import numpy as np
     import torch
     dev = rank % torch.cuda.device_count()  # GPU r; both on GPU 0 when rehearsing on a one-GPU box
     torch.cuda.set_device(dev)
@@ -115,7 +114,6 @@ def ring_rank(rank: int, shm: str, counts) -> int:
                                    "exact": bool(torch.equal(y, exp))}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    del np
     return 0
 
 
