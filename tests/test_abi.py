@@ -184,3 +184,15 @@ def test_peer_ring_rejects_bad_configs_before_the_device():
         cfg = ring.PeerRingConfig(**f)
         assert L.nexrPeerRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)) == 4, bad
     assert L.nexrPeerRingAllReduce(None, None, None, 0, 7, 0) == 4
+
+
+def test_c_example_builds_with_plain_c(tmp_path):
+    """include/nexr.h and include/nexr_ring.h are plain C: the example host program (the fork's C
+    host code's view of the boundary) compiles and links with gcc -std=c11 -Wall -Wextra -Werror."""
+    import subprocess
+    out = tmp_path / "reduce_copy_c"
+    lib = os.path.join(ROOT, "nex-nccl_amd")
+    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I" + os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "reduce_copy_c.c"), "-L" + lib, "-lnexr_ring", "-lnexr",
+                    "-Wl,-rpath," + lib, "-o", str(out)], check=True, capture_output=True, text=True, timeout=120)
+    assert out.exists()
