@@ -153,8 +153,9 @@ NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int n
  * nexrReduceCopyHost — the same reduce-copy for buffers in HOST memory (the emulated
  * transport's staging FIFOs, reference src/include/device.h:753-771): copies the K inputs
  * host->device, runs nexrReduceCopy, copies the M outputs device->host, and synchronises the
- * stream before returning. Device scratch is taken from a per-device cache grown on demand
- * (the only call that may allocate). When every buffer is pinned host memory (hipHostMalloc /
+ * stream before returning. Device scratch is a staging ring checked out of a process-wide,
+ * per-device pool for the duration of the call and handed back at its end (grown on demand; the
+ * only call that may allocate), so callers on short-lived threads reuse the same rings. When every buffer is pinned host memory (hipHostMalloc /
  * hipHostRegister / torch pin_memory) the kernel reads and writes it in place over PCIe (zero-copy,
  * both directions concurrently; NEXR_HOST_ZERO_COPY=0 disables). Otherwise the call stages through
  * device memory in chunks (NEXR_HOST_CHUNK_BYTES, default 8 MiB per buffer): chunk c is copied in

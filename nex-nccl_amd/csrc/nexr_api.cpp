@@ -5,6 +5,9 @@
 #include <string.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <vector>
+
 #include "nexr_internal.h"
 
 namespace nexr {
@@ -240,10 +243,13 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   return nexrSuccess;
 }
 
-// ---- host-staged variant: per-thread, per-device staging ring -----------------------------------
-// Two device slots of (K+1) x chunk bytes; chunk c is copied in (H2D) and reduced on the caller's
-// stream while chunk c-1 is copied out (D2H) on a second stream, so the two PCIe directions run
-// concurrently. Created on first use, grown on demand, kept for the thread's lifetime.
+// ---- host-staged variant: a process-wide pool of staging rings ----------------------------------
+// A ring is two device slots of (K+1) x chunk bytes: chunk c is copied in (H2D) and reduced on the
+// caller's stream while chunk c-1 is copied out (D2H) on the ring's own stream, so the two PCIe
+// directions run concurrently. A call checks a ring out for its duration and hands it back, so the
+// pool holds, per device, as many rings as host calls have ever run there at once. (The emulated
+// collectives run each call's ranks on fresh threads: a ring cached per thread would be a new device
+// allocation and stream per thread, never freed.)
 struct HostStage {
   int device = -1;
   char* buf = nullptr;
@@ -252,37 +258,66 @@ struct HostStage {
   hipEvent_t kernelDone[2] = {nullptr, nullptr};
   hipEvent_t outDone[2] = {nullptr, nullptr};
 };
-thread_local HostStage tStage[8];
+std::mutex gStageMu;
+std::vector<HostStage*> gStageIdle;
 
-nexrResult_t stageFor(size_t slotBytes, HostStage** out) {
+// Checks a ring out for the current device (the largest idle one, or a new one) and hands it back
+// when the call ends. Release drains the ring's stream and the caller's stream first, so that no
+// copy of this call still targets the slots when another call takes the ring; a ring whose streams
+// report an error is dropped rather than reused.
+struct StageLease {
+  HostStage* st = nullptr;
+  hipStream_t caller = nullptr;
+  ~StageLease() {
+    if (!st) return;
+    bool ok = hipStreamSynchronize(st->out) == hipSuccess;
+    ok = hipStreamSynchronize(caller) == hipSuccess && ok;
+    if (!ok) {
+      (void)hipGetLastError();
+      return;
+    }
+    std::lock_guard<std::mutex> g(gStageMu);
+    gStageIdle.push_back(st);
+  }
+};
+
+nexrResult_t stageFor(size_t slotBytes, hipStream_t caller, StageLease* lease) {
   int dev = 0;
   NEXR_HIP(hipGetDevice(&dev));
   HostStage* st = nullptr;
-  for (auto& s : tStage)
-    if (s.device == dev) { st = &s; break; }
-  if (!st)
-    for (auto& s : tStage)
-      if (s.device < 0) { st = &s; break; }
-  if (!st) return nexrSystemError;
-  if (st->device < 0) {
-    NEXR_HIP(hipStreamCreateWithFlags(&st->out, hipStreamNonBlocking));
+  {
+    std::lock_guard<std::mutex> g(gStageMu);
+    size_t best = gStageIdle.size();
+    for (size_t i = 0; i < gStageIdle.size(); i++)
+      if (gStageIdle[i]->device == dev && (best == gStageIdle.size() || gStageIdle[i]->slotBytes > gStageIdle[best]->slotBytes))
+        best = i;
+    if (best < gStageIdle.size()) {
+      st = gStageIdle[best];
+      gStageIdle.erase(gStageIdle.begin() + (long)best);
+    }
+  }
+  if (!st) {
+    st = new HostStage();
+    if (hipStreamCreateWithFlags(&st->out, hipStreamNonBlocking) != hipSuccess) {
+      delete st;
+      return hipFail(hipGetLastError());
+    }
     for (int i = 0; i < 2; i++) {
-      NEXR_HIP(hipEventCreateWithFlags(&st->kernelDone[i], hipEventDisableTiming));
-      NEXR_HIP(hipEventCreateWithFlags(&st->outDone[i], hipEventDisableTiming));
+      if (hipEventCreateWithFlags(&st->kernelDone[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&st->outDone[i], hipEventDisableTiming) != hipSuccess)
+        return hipFail(hipGetLastError());  // the half-built ring is not pooled
     }
     st->device = dev;
   }
-  if (st->slotBytes < slotBytes) {
-    if (st->buf) {
-      NEXR_HIP(hipStreamSynchronize(st->out));
-      NEXR_HIP(hipFree(st->buf));
-    }
+  lease->st = st;
+  lease->caller = caller;
+  if (st->slotBytes < slotBytes) {  // idle ring: its stream was drained when it was handed back
+    if (st->buf) NEXR_HIP(hipFree(st->buf));
     st->buf = nullptr;
     st->slotBytes = 0;
     NEXR_HIP(hipMalloc((void**)&st->buf, 2 * slotBytes));
     st->slotBytes = slotBytes;
   }
-  *out = st;
   return nexrSuccess;
 }
 
@@ -382,9 +417,10 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
   size_t chunkElts = ((size_t)(chunkOverride > 4096 ? chunkOverride : 4096) / esz) & ~(size_t)15;
   if (chunkElts > nElts) chunkElts = nElts;
   const size_t chunkBytes = ((chunkElts * esz) + 255) & ~(size_t)255;
-  HostStage* st = nullptr;
-  r = stageFor(chunkBytes * (size_t)(nSrcs + 1), &st);
+  StageLease lease;
+  r = stageFor(chunkBytes * (size_t)(nSrcs + 1), s, &lease);
   if (r != nexrSuccess) return r;
+  HostStage* st = lease.st;
   bool anyPageableDst = false;
   for (int d = 0; d < nDsts; d++) anyPageableDst |= !pdst[d];
   const size_t nChunks = (nElts + chunkElts - 1) / chunkElts;

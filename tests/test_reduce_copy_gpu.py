@@ -328,6 +328,47 @@ def test_host_staged_pipeline_multi_chunk(nexr, oracle, dt, n, op, name, dev):
         assert same(dt, d, exp)
 
 
+def test_host_staging_rings_are_pooled_not_per_thread(nexr, oracle, dev):
+    """Callers such as the emulated collectives run every call's ranks on fresh threads. Each
+    host-staged call checks a staging ring out of a process-wide pool and returns it, so 40 calls
+    from 40 short-lived threads (and 8 at once) reuse a bounded set of rings: device memory must not
+    grow by one ring (here 2 x 3 x 4 MiB) per thread."""
+    n = 1_000_003
+    srcs = mg.gen_inputs(mg.F32, 2, n, 4242, special=True)
+    exp = oracle.reduce_copy(srcs, 1, mg.F32, mg.SUM)[0]
+    sp = [s.ctypes.data for s in srcs]
+    errors = []
+
+    def call():
+        try:
+            torch.cuda.set_device(0)
+            d = np.zeros_like(srcs[0])
+            nexr.reduce_copy_ptrs(sp, [d.ctypes.data], n, mg.F32, mg.SUM, host=True)
+            if not same(mg.F32, d, exp):
+                errors.append("mismatch")
+        except Exception as e:  # noqa: BLE001 - collected and asserted below
+            errors.append(repr(e))
+
+    def run_threads(k):
+        ths = [threading.Thread(target=call) for _ in range(k)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+
+    run_threads(1)  # the pool's first ring
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    for _ in range(40):
+        run_threads(1)
+    for _ in range(3):
+        run_threads(8)
+    torch.cuda.synchronize()
+    grown = free0 - torch.cuda.mem_get_info(0)[0]
+    assert not errors, errors[:3]
+    ring = 2 * 3 * (4 << 20)
+    # at most the 7 extra rings the 8-way rounds need (one ring per concurrent call), never one per thread
+    assert grown <= 8 * ring, f"device memory grew by {grown / 2**20:.0f} MiB over 64 host-staged threads"
+
+
 def test_host_zero_copy_pinned_buffers(nexr, oracle, dev):
     # pinned (device-mapped) host buffers: the kernel reads/writes them in place over PCIe;
     # interior pointers (offset into the allocation) and a pinned/pageable mix (-> staged) too.
