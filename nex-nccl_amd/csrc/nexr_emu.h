@@ -33,6 +33,26 @@ struct Geom {
 constexpr Geom kGeomRing{kSteps / 2, kSteps / 4};  // ALLREDUCE/ALLGATHER/REDUCESCATTER_*STEPS
 constexpr Geom kGeomPipe{1, 1};                    // BROADCAST/REDUCE_*STEPS; the tree's ProtoSimple<1,1>
 
+// Keeps the calling thread's current HIP device across an entry point, as NCCL's entry points keep
+// the caller's CUDA device (init.cc:1873 ncclCommInitAll, enqueue.cc:2422 ncclEnqueueCheck). The
+// entry points select each rank's device while they build streams and FIFOs or run a process rank's
+// steps; without the guard the caller (and PyTorch, whose current device is HIP's) would be left on
+// the last rank's device. Inactive for communicators that never touch HIP (CPU checkers).
+struct DeviceGuard {
+  int dev = -1;
+  explicit DeviceGuard(bool active) {
+    if (active && hipGetDevice(&dev) != hipSuccess) {
+      (void)hipGetLastError();
+      dev = -1;
+    }
+  }
+  ~DeviceGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 // One directed connection. The FIFO belongs to the receiver (the sender writes into it, like a
 // P2P/SHM transport's recv buffer, src/include/device.h:753-771).
 struct ConnState {

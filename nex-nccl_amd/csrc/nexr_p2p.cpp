@@ -131,10 +131,12 @@ extern "C" {
 
 NEXR_API nexrResult_t nexrSendRecv(nexrRingComm_t c, const void* const* sendbuffs, const int* sendPeers,
                                    void* const* recvbuffs, const int* recvPeers, size_t bytes) {
+  DeviceGuard dg(c && c->needHip);
   return sendRecv(c, sendbuffs, sendPeers, recvbuffs, recvPeers, bytes);
 }
 NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t c, const void* sendbuff, int sendPeer, void* recvbuff,
                                        int recvPeer, size_t bytes) {
+  DeviceGuard dg(c && c->needHip);
   if (!c || !c->peer) return nexrInvalidArgument;
   if (c->broken) return nexrInvalidUsage;
   if (c->proto != nexrRingProtoSimple) return nexrInvalidUsage;

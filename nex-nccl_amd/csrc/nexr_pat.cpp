@@ -692,11 +692,13 @@ extern "C" {
 
 NEXR_API nexrResult_t nexrPatReduceScatter(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                            size_t recvcount, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   return patCollective(c, true, sendbuffs, recvbuffs, recvcount, datatype, op);
 }
 
 NEXR_API nexrResult_t nexrPatAllGather(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                        size_t sendcount, int datatype) {
+  DeviceGuard dg(c && c->needHip);
   return patCollective(c, false, sendbuffs, recvbuffs, sendcount, datatype, nexrSum);  // ncclAllGather: ncclSum
 }
 NEXR_API nexrResult_t nexrPatSchedule(int reduceScatter, int nRanks, int rank, size_t count, int datatype,
@@ -709,11 +711,13 @@ NEXR_API nexrResult_t nexrPatSchedule(int reduceScatter, int nRanks, int rank, s
 }
 NEXR_API nexrResult_t nexrPeerPatReduceScatter(nexrRingComm_t c, const void* sendbuff, void* recvbuff,
                                                size_t recvcount, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   return peerPat(c, true, sendbuff, recvbuff, recvcount, datatype, op);
 }
 
 NEXR_API nexrResult_t nexrPeerPatAllGather(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t sendcount,
                                            int datatype) {
+  DeviceGuard dg(c && c->needHip);
   return peerPat(c, false, sendbuff, recvbuff, sendcount, datatype, nexrSum);
 }
 

@@ -673,11 +673,19 @@ nexrResult_t peerFinish(nexrRingComm* c, Shared& sh) {
   return nexrSuccess;
 }
 
+// A communicator touches HIP when its FIFOs live in device memory or when any of its steps runs the
+// built-in (HIP) reduce-copy; one whose steps are all caller-supplied (a CPU checker) never does.
+bool needsHip(const nexrRingConfig& cfg) {
+  return cfg.memMode == nexrRingDeviceMemory || (cfg.protocol == nexrRingProtoSimple && !cfg.fn) ||
+         (cfg.protocol == nexrRingProtoLL && !cfg.llFn) || (cfg.protocol == nexrRingProtoLL128 && !cfg.ll128Fn);
+}
+
 }  // namespace nexr_emu
 
 extern "C" {
 
 NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConfig* cfg) {
+  DeviceGuard dg(cfg && needsHip(*cfg));
   if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024) return nexrInvalidArgument;
   if (cfg->memMode != nexrRingHostMemory && cfg->memMode != nexrRingDeviceMemory) return nexrInvalidArgument;
   if (cfg->protocol != nexrRingProtoSimple && cfg->protocol != nexrRingProtoLL && cfg->protocol != nexrRingProtoLL128)
@@ -715,8 +723,7 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   c->streams.assign(n, nullptr);
   c->status.assign(n, nullptr);
   int nDev = 0;
-  c->needHip = cfg->memMode == nexrRingDeviceMemory || (c->proto == nexrRingProtoSimple && !cfg->fn) ||
-               (c->proto == nexrRingProtoLL && !cfg->llFn) || (c->proto == nexrRingProtoLL128 && !cfg->ll128Fn);
+  c->needHip = needsHip(*cfg);
   c->pinnedStatus = c->needHip;
   if (c->needHip) {
     if (hipGetDeviceCount(&nDev) != hipSuccess || nDev < 1) {
@@ -770,31 +777,37 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
 
 NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   return ringCollective(c, kAllReduce, sendbuffs, recvbuffs, count, datatype, op, 0);
 }
 
 NEXR_API nexrResult_t nexrRingReduceScatter(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                             size_t recvcount, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   return ringCollective(c, kReduceScatter, sendbuffs, recvbuffs, recvcount, datatype, op, 0);
 }
 
 NEXR_API nexrResult_t nexrRingAllGather(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t sendcount, int datatype) {
+  DeviceGuard dg(c && c->needHip);
   return ringCollective(c, kAllGather, sendbuffs, recvbuffs, sendcount, datatype, nexrSum, 0);  // ncclAllGather: ncclSum
 }
 
 NEXR_API nexrResult_t nexrRingReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                      size_t count, int datatype, int op, int root) {
+  DeviceGuard dg(c && c->needHip);
   return ringCollective(c, kReduce, sendbuffs, recvbuffs, count, datatype, op, root);
 }
 
 NEXR_API nexrResult_t nexrRingBroadcast(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int root) {
+  DeviceGuard dg(c && c->needHip);
   return ringCollective(c, kBroadcast, sendbuffs, recvbuffs, count, datatype, nexrSum, root);  // ncclBroadcast: ncclSum
 }
 
 NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   if (!c || c->peer) return nexrInvalidArgument;
   size_t esz;
   nexrDevRedOpFull red;
@@ -872,6 +885,7 @@ NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t c, int rank, int* up, int*
 }
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
+  DeviceGuard dg(c && c->needHip);
   if (!c) return nexrInvalidArgument;
   for (nexrRingComm* ch : c->channels) nexrRingCommDestroy(ch);
   c->channels.clear();
@@ -929,6 +943,7 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
 // tail counters pair up as in p2pSendConnect/p2pRecvConnect (:514-515, :542-543). Here the steps are
 // driven by each rank's host thread, so the counters live in host shared memory.
 NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeerRingConfig* cfg) {
+  DeviceGuard dg(true);
   if (!out || !cfg || cfg->nRanks < 1 || cfg->nRanks > 1024 || cfg->rank < 0 || cfg->rank >= cfg->nRanks)
     return nexrInvalidArgument;
   if (!cfg->shmName || cfg->shmName[0] != '/' || strlen(cfg->shmName) >= 255 || strchr(cfg->shmName + 1, '/'))
@@ -1047,26 +1062,31 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
 
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   return peerCollective(c, kAllReduce, sendbuff, recvbuff, count, datatype, op, 0);
 }
 
 NEXR_API nexrResult_t nexrPeerRingReduceScatter(nexrRingComm_t c, const void* sendbuff, void* recvbuff,
                                                 size_t recvcount, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
   return peerCollective(c, kReduceScatter, sendbuff, recvbuff, recvcount, datatype, op, 0);
 }
 
 NEXR_API nexrResult_t nexrPeerRingAllGather(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t sendcount,
                                             int datatype) {
+  DeviceGuard dg(c && c->needHip);
   return peerCollective(c, kAllGather, sendbuff, recvbuff, sendcount, datatype, nexrSum, 0);
 }
 
 NEXR_API nexrResult_t nexrPeerRingReduce(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
                                          int datatype, int op, int root) {
+  DeviceGuard dg(c && c->needHip);
   return peerCollective(c, kReduce, sendbuff, recvbuff, count, datatype, op, root);
 }
 
 NEXR_API nexrResult_t nexrPeerRingBroadcast(nexrRingComm_t c, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int root) {
+  DeviceGuard dg(c && c->needHip);
   return peerCollective(c, kBroadcast, sendbuff, recvbuff, count, datatype, nexrSum, root);
 }
 

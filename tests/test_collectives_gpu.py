@@ -151,3 +151,32 @@ def test_mixed_slice_geometries_on_one_device_comm(ring, oracle):
                 assert rs[r].cpu().numpy().tobytes() == e.tobytes()
             e = reduce_expected([v[:count - it] for v in x], dt, 0, 1)
             assert red[1].cpu().numpy()[:count - it].tobytes() == e.tobytes()
+
+
+def test_caller_device_survives_multi_gpu_comm(ring, oracle):
+    """Rank r of a device-memory communicator lives on GPU r % nDev, and the entry points select each
+    rank's device while they build its stream and FIFO. The caller's current device (PyTorch's too)
+    must be the same after create, the collectives and destroy, as NCCL keeps it (init.cc:1873,
+    enqueue.cc:2422). Needs two GPUs: skipped on the one-GPU box, runs on a multi-GPU node."""
+    n_dev = torch.cuda.device_count()
+    if n_dev < 2:
+        pytest.skip("needs 2 GPUs")
+    n, count = n_dev, 70_001
+    inputs = mg.gen_inputs(mg.I32, n, count, 0x5151, False)
+    for home in (0, n_dev - 1):
+        torch.cuda.set_device(home)
+        send = [torch.from_numpy(a.copy()).to(f"cuda:{r}") for r, a in enumerate(inputs)]
+        recv = [torch.zeros_like(t) for t in send]
+        for t in send:
+            torch.cuda.synchronize(t.device)
+        with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 18) as comm:
+            assert torch.cuda.current_device() == home, "nexrRingCommCreate moved the caller's device"
+            comm.all_reduce(_ptrs(send), _ptrs(recv), count, mg.I32, 0)
+            assert torch.cuda.current_device() == home, "nexrRingAllReduce moved the caller's device"
+            comm.tree_all_reduce(_ptrs(send), _ptrs(recv), count, mg.I32, 0)
+            assert torch.cuda.current_device() == home, "nexrTreeAllReduce moved the caller's device"
+        assert torch.cuda.current_device() == home, "nexrRingCommDestroy moved the caller's device"
+        exp = np.sum(np.stack(inputs).astype(np.int64), axis=0).astype(np.int32)  # wrapping int32 sum, any order
+        for r in range(n):
+            assert np.array_equal(recv[r].cpu().numpy(), exp), f"rank {r}"
+    torch.cuda.set_device(0)
