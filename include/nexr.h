@@ -150,6 +150,22 @@ NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int n
                                           nexrStream_t stream);
 
 /*
+ * nexrReduceCopyMultiDevice — independent reduce-copies on several GPUs of one node from one host
+ * call: the independent-chunk sharding of SURVEY §8(e) (config C5) as a native host driver, with no
+ * collective and no peer access. Work i runs on HIP device devices[i] (its buffers live there) on a
+ * host thread of its own: hipSetDevice, a non-blocking stream of its own, a start barrier shared by
+ * all works, then `reps` reduce-copies (each exactly one nexrReduceCopy of work i) and
+ * hipStreamSynchronize. Every work and device ordinal is validated before any thread starts; the
+ * first error of any work is returned. When `seconds` is non-null it receives the wall time from the
+ * barrier's release to the last device's completion. The caller's current device is unchanged. Works
+ * must not overlap one another (in-place within one work is allowed). At most
+ * NEXR_MAX_MULTI_DEVICE_WORKS works; several may name the same device.
+ */
+#define NEXR_MAX_MULTI_DEVICE_WORKS 64
+NEXR_API nexrResult_t nexrReduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks,
+                                                int datatype, int devRedOp, int reps, double* seconds);
+
+/*
  * nexrReduceCopyHost — the same reduce-copy for buffers in HOST memory (the emulated
  * transport's staging FIFOs, reference src/include/device.h:753-771): copies the K inputs
  * host->device, runs nexrReduceCopy, copies the M outputs device->host, and synchronises the

@@ -76,7 +76,7 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
              DataType.Float8e5m2: 1}
 
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
-ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
+ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
                "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
 
 
@@ -126,6 +126,8 @@ def lib() -> ctypes.CDLL:
         f.restype = i32
     L.nexrReduceCopyBatch.argtypes = [P(ReduceCopyWork), i32, i32, i32, vp]
     L.nexrReduceCopyBatch.restype = i32
+    L.nexrReduceCopyMultiDevice.argtypes = [P(ReduceCopyWork), P(i32), i32, i32, i32, i32, P(ctypes.c_double)]
+    L.nexrReduceCopyMultiDevice.restype = i32
     L.nexrHostToDevRedOp.argtypes = [P(DevRedOpFull), i32, i32, i32]
     L.nexrHostToDevRedOp.restype = i32
     L.nexrLaunchOneRank.argtypes = [vp, vp, sz, DevRedOpFull, i32, vp]
@@ -214,6 +216,21 @@ def reduce_copy_batch(works: Sequence[ReduceCopyWork], datatype: int, dev_red_op
     arr = (ReduceCopyWork * max(1, len(works)))(*works)
     _check(lib().nexrReduceCopyBatch(arr, len(works), int(datatype), int(dev_red_op),
                                      ctypes.c_void_p(int(stream)) if stream else None), "nexrReduceCopyBatch")
+
+
+def reduce_copy_multi_device(works: Sequence[ReduceCopyWork], devices: Sequence[int], datatype: int,
+                             dev_red_op: int, reps: int = 1) -> float:
+    """``nexrReduceCopyMultiDevice``: work i on GPU devices[i], one host thread and stream per work,
+    a shared start barrier, `reps` launches each. Returns seconds from the barrier to the last
+    device's completion."""
+    if len(works) != len(devices):
+        raise NexrError(Result.InvalidArgument, "one device per work")
+    arr = (ReduceCopyWork * max(1, len(works)))(*works)
+    dev = (ctypes.c_int * max(1, len(devices)))(*[int(d) for d in devices])
+    secs = ctypes.c_double(0.0)
+    _check(lib().nexrReduceCopyMultiDevice(arr, dev, len(works), int(datatype), int(dev_red_op), int(reps),
+                                           ctypes.byref(secs)), "nexrReduceCopyMultiDevice")
+    return secs.value
 
 
 def host_to_dev_red_op(op: int, datatype: int, n_ranks: int = 1) -> DevRedOpFull:

@@ -5,7 +5,10 @@
 #include <string.h>
 #include <stdlib.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "nexr_internal.h"
@@ -243,6 +246,83 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   return nexrSuccess;
 }
 
+// ---- independent chunks on several GPUs from one host call -------------------
+// One host thread per work: hipSetDevice, a stream of its own, the shared start barrier, `reps`
+// launches, hipStreamSynchronize. A thread whose setup fails still arrives at the barrier (so the
+// others are released) and reports its error.
+nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks, int datatype,
+                                   int op, int reps, double* seconds) {
+  if (nWorks < 0 || nWorks > NEXR_MAX_MULTI_DEVICE_WORKS || reps < 1) return nexrInvalidArgument;
+  if (nWorks > 0 && (works == nullptr || devices == nullptr)) return nexrInvalidArgument;
+  for (int i = 0; i < nWorks; i++) {
+    const nexrReduceCopyWork& w = works[i];
+    nexrResult_t r = validate(w.nSrcs, w.srcs, w.nDsts, w.dsts, w.nElts, datatype, op, w.redOpArg, w.nPreOpSrcs,
+                              w.preOpArgs);
+    if (r != nexrSuccess) return r;
+  }
+  if (seconds) *seconds = 0.0;
+  if (nWorks == 0) return nexrSuccess;
+  int nDev = 0;
+  NEXR_HIP(hipGetDeviceCount(&nDev));
+  for (int i = 0; i < nWorks; i++)
+    if (devices[i] < 0 || devices[i] >= nDev) return nexrInvalidArgument;
+
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  std::chrono::steady_clock::time_point t0;
+  std::vector<std::chrono::steady_clock::time_point> t1(nWorks);
+  std::vector<nexrResult_t> res(nWorks, nexrSuccess);
+  std::vector<int> hipErr(nWorks, 0);
+  auto run = [&](int i) {
+    const nexrReduceCopyWork& w = works[i];
+    hipStream_t st = nullptr;
+    hipError_t e = hipSetDevice(devices[i]);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      res[i] = nexrUnhandledCudaError;
+      hipErr[i] = (int)e;
+    }
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      if (++arrived == nWorks) {
+        t0 = std::chrono::steady_clock::now();
+        cv.notify_all();
+      } else {
+        cv.wait(lk, [&] { return arrived == nWorks; });
+      }
+    }
+    for (int k = 0; k < reps && res[i] == nexrSuccess; k++)
+      res[i] = reduceCopyDevice(w.nSrcs, w.srcs, w.nDsts, w.dsts, w.nElts, datatype, op, w.redOpArg, w.nPreOpSrcs,
+                                w.preOpArgs, nullptr, w.postOp, st);
+    if (res[i] == nexrUnhandledCudaError && hipErr[i] == 0) hipErr[i] = tLastHipError;
+    if (st) {
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess && res[i] == nexrSuccess) {
+        res[i] = nexrUnhandledCudaError;
+        hipErr[i] = (int)e;
+      }
+      (void)hipStreamDestroy(st);
+    }
+    t1[i] = std::chrono::steady_clock::now();
+  };
+  std::vector<std::thread> threads;
+  threads.reserve(nWorks);
+  for (int i = 0; i < nWorks; i++) threads.emplace_back(run, i);
+  for (auto& t : threads) t.join();
+  for (int i = 0; i < nWorks; i++)
+    if (res[i] != nexrSuccess) {
+      tLastHipError = hipErr[i];
+      return res[i];
+    }
+  if (seconds) {
+    auto last = t1[0];
+    for (int i = 1; i < nWorks; i++) last = t1[i] > last ? t1[i] : last;
+    *seconds = std::chrono::duration<double>(last - t0).count();
+  }
+  return nexrSuccess;
+}
+
 // ---- host-staged variant: a process-wide pool of staging rings ----------------------------------
 // A ring is two device slots of (K+1) x chunk bytes: chunk c is copied in (H2D) and reduced on the
 // caller's stream while chunk c-1 is copied out (D2H) on the ring's own stream, so the two PCIe
@@ -370,6 +450,11 @@ NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDs
 NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int devRedOp,
                                           nexrStream_t stream) {
   return reduceCopyBatch(works, nWorks, datatype, devRedOp, (hipStream_t)stream);
+}
+
+NEXR_API nexrResult_t nexrReduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks,
+                                                int datatype, int devRedOp, int reps, double* seconds) {
+  return reduceCopyMultiDevice(works, devices, nWorks, datatype, devRedOp, reps, seconds);
 }
 
 NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,

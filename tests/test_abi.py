@@ -129,6 +129,25 @@ def test_batch_validates_every_work_before_launching(nexr):
         nexr.make_work([1] * 9, [2], 4)
 
 
+def test_multi_device_validates_before_any_thread(nexr):
+    L = nexr.lib()
+    good = nexr.make_work([0x1000, 0x2000], [0x3000], 16)
+    bad = nexr.make_work([0x1000, 0], [0x3000], 16)
+    dev = (ctypes.c_int * 3)(0, 0, 0)
+    secs = ctypes.c_double(-1.0)
+    arr = (nexr.ReduceCopyWork * 3)(good, bad, good)
+    assert L.nexrReduceCopyMultiDevice(arr, dev, 3, 7, 0, 1, ctypes.byref(secs)) == 4
+    arr = (nexr.ReduceCopyWork * 1)(good)
+    assert L.nexrReduceCopyMultiDevice(arr, dev, 1, 7, 0, 0, None) == 4     # reps < 1
+    assert L.nexrReduceCopyMultiDevice(arr, None, 1, 7, 0, 1, None) == 4    # no device list
+    assert L.nexrReduceCopyMultiDevice(arr, dev, 1, 11, 0, 1, None) == 4    # fp8
+    assert L.nexrReduceCopyMultiDevice(arr, dev, 65, 7, 0, 1, None) == 4    # > NEXR_MAX_MULTI_DEVICE_WORKS
+    assert L.nexrReduceCopyMultiDevice(None, None, 0, 7, 0, 1, ctypes.byref(secs)) == 0
+    assert secs.value == 0.0
+    with pytest.raises(nexr.NexrError):
+        nexr.reduce_copy_multi_device([good], [0, 1], 7, 0)
+
+
 @pytest.mark.parametrize("dt", sorted(mg.DT_NAMES) + [10, 11])
 @pytest.mark.parametrize("op,nranks", [(0, 2), (1, 2), (2, 4), (3, 4), (4, 1), (4, 3), (4, 8), (5, 2)])
 def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):

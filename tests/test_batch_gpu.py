@@ -139,3 +139,43 @@ def test_batch_equals_separate_calls_bitwise(nexr, dev):
     torch.cuda.synchronize()
     for a, b in zip(outs_b, outs_s):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+
+
+@pytest.mark.parametrize("dt", [mg.F32, mg.BF16, mg.I8, mg.F64])
+def test_multi_device_independent_chunks_match_oracle(nexr, oracle, dt, dev):
+    """nexrReduceCopyMultiDevice (SURVEY §8(e), C5's independent chunks from one host call): every
+    work on its own host thread and stream after a shared start barrier. On the one-GPU box every
+    work names device 0 (several threads on one device); on a multi-GPU node work i takes GPU i mod n.
+    Every work (all ops, mixed K/M/sizes/phases, reps > 1) against the oracle, guard bytes intact, the
+    caller's current device unchanged."""
+    rng = np.random.default_rng(500 + dt)
+    n_dev = torch.cuda.device_count()
+    for name, op in OPS:
+        if name == "sumpostdiv" and dt not in mg.INTS:
+            continue
+        works = []
+        for w in range(int(rng.choice([1, 3, 8]))):
+            k, m = int(rng.integers(1, 9)), int(rng.integers(1, 3))
+            n = int(rng.choice([0, 17, 4097, 300_001, 2_000_003]))
+            d = w % n_dev
+            with torch.cuda.device(d):
+                works.append((_Work(nexr, oracle, dt, op, name, k, m, n, 7000 + 31 * w + op, rng,
+                                    ["zero", "phase", "random"][w % 3]), d))
+        torch.cuda.synchronize()
+        before = torch.cuda.current_device()
+        secs = nexr.reduce_copy_multi_device([w.work for w, _ in works], [d for _, d in works], dt, op,
+                                             reps=int(rng.integers(1, 4)))
+        assert torch.cuda.current_device() == before
+        assert secs >= 0.0
+        for i, (w, _) in enumerate(works):
+            w.check((mg.DT_NAMES[dt], name, i, w.n))
+
+
+def test_multi_device_rejects_bad_ordinals(nexr, dev):
+    x = torch.ones(1024, device="cuda")
+    y = torch.empty_like(x)
+    work = nexr.make_work([x.data_ptr(), x.data_ptr()], [y.data_ptr()], 1024)
+    for bad in (-1, torch.cuda.device_count()):
+        with pytest.raises(nexr.NexrError) as e:
+            nexr.reduce_copy_multi_device([work], [bad], mg.F32, 0)
+        assert e.value.code == 4
