@@ -96,6 +96,17 @@ class Dist:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, values, device=None) -> list:
+        """Every rank's `values` (a list of floats of one length), indexed by rank; harness only."""
+        if not self.pg:
+            return [list(values)]
+        import torch
+        dev = device if self.backend == "nccl" else None
+        t = torch.tensor(values, dtype=torch.float64, device=dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.pg.all_gather(out, t)
+        return [o.tolist() for o in out]
+
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
@@ -235,6 +246,8 @@ def main(argv=None):
     value = dist.world * bytes_step * args.steps / max_s / 1e9
     achieved = bytes_step / avg_kernel_s / 1e9
     traffic, traffic_src = load_traffic(args.config)
+    # per-GPU rates beside the aggregate (every rank's own wall time and kernel time).
+    ranks = dist.gather([local_s, avg_kernel_s], dev)
 
     result = None
     if dist.rank == 0:
@@ -276,11 +289,23 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d,
         }
+        if dist.world > 1:
+            result["per_gpu"] = per_gpu_summary(ranks, bytes_step, args.steps)
         if xgmi is not None:
             result["xgmi_probe"] = xgmi
         print(json.dumps(result), flush=True)
     dist.close()
     return result
+
+
+def per_gpu_summary(ranks, bytes_step: int, steps: int) -> dict:
+    """Per-rank wall and kernel rates of an N > 1 run: `ranks[r] = [wall seconds, kernel seconds per
+    launch]`. `value` stays the aggregate (N x bytes / max wall); this shows how even the ranks were."""
+    wall = [bytes_step * steps / w / 1e9 for w, _ in ranks]
+    kern = [bytes_step / k / 1e9 if k > 0 else 0.0 for _, k in ranks]
+    return {"value": round(sum(wall) / len(wall), 2), "unit": "GB/s",
+            "wall_gbs": [round(x, 1) for x in wall], "kernel_gbs": [round(x, 1) for x in kern],
+            "min_wall_gbs": round(min(wall), 2), "max_wall_gbs": round(max(wall), 2)}
 
 
 def xgmi_probe(timeout_s: float = 150.0):

@@ -40,8 +40,10 @@ def _rank_main(rank, world, port, q):
 
     local, mx = bench.timed_steps(step, steps=5, warmup=1, sync=lambda: None, dist=d)
     ok = np.array_equal(out[0], (srcs[0] + srcs[1]).astype(np.float32))
+    gathered = d.gather([local, float(rank)])
+    summary = bench.per_gpu_summary(gathered, bytes_step=1 << 20, steps=5)
     d.close()
-    q.put((rank, local, mx, ok))
+    q.put((rank, local, mx, ok, gathered, summary))
 
 
 def test_two_rank_independent_chunks_max_timer():
@@ -53,7 +55,11 @@ def test_two_rank_independent_chunks_max_timer():
     res = sorted(q.get(timeout=120) for _ in ps)
     [p.join(timeout=60) for p in ps]
     assert all(p.exitcode == 0 for p in ps)
-    (r0, l0, m0, ok0), (r1, l1, m1, ok1) = res
+    (r0, l0, m0, ok0, g0, s0), (r1, l1, m1, ok1, g1, s1) = res
     assert ok0 and ok1
     assert m0 == m1 == max(l0, l1)
     assert l1 >= 0.05  # the skewed rank's 5 steps
+    # per-rank breakdown of the N > 1 bench line: every rank sees every rank's time, in rank order
+    assert g0 == g1 == [[l0, 0.0], [l1, 1.0]]
+    assert s0 == s1 and len(s0["wall_gbs"]) == 2
+    assert s0["min_wall_gbs"] == round(5 * (1 << 20) / l1 / 1e9, 2)  # the slow rank sets the minimum
