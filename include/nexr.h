@@ -153,8 +153,8 @@ NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int n
  * nexrReduceCopyMultiDevice — independent reduce-copies on several GPUs of one node from one host
  * call: the independent-chunk sharding of SURVEY §8(e) (config C5) as a native host driver, with no
  * collective and no peer access. Work i runs on HIP device devices[i] (its buffers live there) on a
- * host thread of its own: hipSetDevice, a non-blocking stream of its own, a start barrier shared by
- * all works, then `reps` reduce-copies (each exactly one nexrReduceCopy of work i) and
+ * host thread of its own: hipSetDevice, a non-blocking stream of its own (checked out of a
+ * process-wide per-device pool and handed back drained), a start barrier shared by all works, then `reps` reduce-copies (each exactly one nexrReduceCopy of work i) and
  * hipStreamSynchronize. Every work and device ordinal is validated before any thread starts; the
  * first error of any work is returned. When `seconds` is non-null it receives the wall time from the
  * barrier's release to the last device's completion. The caller's current device is unchanged. Works

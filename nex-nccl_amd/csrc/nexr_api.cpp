@@ -250,6 +250,29 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
 // One host thread per work: hipSetDevice, a stream of its own, the shared start barrier, `reps`
 // launches, hipStreamSynchronize. A thread whose setup fails still arrives at the barrier (so the
 // others are released) and reports its error.
+// Streams come from a process-wide per-device pool: a stream is checked out for one work of one
+// call and handed back drained. (A fresh stream per call cost ~1.5 ms on its first launches, which
+// dominated calls of tens of MiB; profiles/r01s5_c_examples_gpu.txt.)
+std::mutex gMdStreamMu;
+std::vector<std::pair<int, hipStream_t>> gMdStreamIdle;
+
+hipError_t mdStreamTake(int dev, hipStream_t* st) {
+  {
+    std::lock_guard<std::mutex> g(gMdStreamMu);
+    for (size_t i = 0; i < gMdStreamIdle.size(); i++)
+      if (gMdStreamIdle[i].first == dev) {
+        *st = gMdStreamIdle[i].second;
+        gMdStreamIdle.erase(gMdStreamIdle.begin() + (long)i);
+        return hipSuccess;
+      }
+  }
+  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
+void mdStreamGive(int dev, hipStream_t st) {  // st was synchronised without error
+  std::lock_guard<std::mutex> g(gMdStreamMu);
+  gMdStreamIdle.emplace_back(dev, st);
+}
 nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks, int datatype,
                                    int op, int reps, double* seconds) {
   if (nWorks < 0 || nWorks > NEXR_MAX_MULTI_DEVICE_WORKS || reps < 1) return nexrInvalidArgument;
@@ -278,7 +301,7 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
     const nexrReduceCopyWork& w = works[i];
     hipStream_t st = nullptr;
     hipError_t e = hipSetDevice(devices[i]);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = mdStreamTake(devices[i], &st);
     if (e != hipSuccess) {
       res[i] = nexrUnhandledCudaError;
       hipErr[i] = (int)e;
@@ -298,13 +321,16 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
     if (res[i] == nexrUnhandledCudaError && hipErr[i] == 0) hipErr[i] = tLastHipError;
     if (st) {
       e = hipStreamSynchronize(st);
+      t1[i] = std::chrono::steady_clock::now();
       if (e != hipSuccess && res[i] == nexrSuccess) {
         res[i] = nexrUnhandledCudaError;
         hipErr[i] = (int)e;
       }
-      (void)hipStreamDestroy(st);
+      if (e == hipSuccess) mdStreamGive(devices[i], st);
+      else (void)hipStreamDestroy(st);
+    } else {
+      t1[i] = std::chrono::steady_clock::now();
     }
-    t1[i] = std::chrono::steady_clock::now();
   };
   std::vector<std::thread> threads;
   threads.reserve(nWorks);

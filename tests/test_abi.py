@@ -215,3 +215,11 @@ def test_c_example_builds_with_plain_c(tmp_path):
                     os.path.join(ROOT, "examples", "reduce_copy_c.c"), "-L" + lib, "-lnexr_ring", "-lnexr",
                     "-Wl,-rpath," + lib, "-o", str(out)], check=True, capture_output=True, text=True, timeout=120)
     assert out.exists()
+
+
+def test_multi_device_c_example_builds(monkeypatch):
+    """examples/multi_device_c.c (C5 from plain C through nexrReduceCopyMultiDevice, device memory from
+    the HIP runtime's C API) compiles and links with gcc -std=c11 -Wall -Wextra -Werror."""
+    import __graft_entry__
+    exe = __graft_entry__.build_c_multi_device()
+    assert os.path.exists(exe) and os.access(exe, os.X_OK)

@@ -17,3 +17,17 @@ def test_c_host_program():
         exe = __graft_entry__.build_c_example()
     p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "reduce_copy_c ok" in p.stdout, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("args", [("64", "5", "1"), ("32", "3", "3"), ("256", "20", "1")])
+def test_c_multi_device_program(args):
+    """C5 from plain C: one independent fp32 sum K=2 reduce-copy per work on every visible GPU from
+    one nexrReduceCopyMultiDevice call (several works per device in the second case), every output
+    checked against a + b on the host."""
+    exe = os.path.join(ROOT, "xbin", "multi_device_c")
+    if not os.path.exists(exe):
+        import __graft_entry__
+        exe = __graft_entry__.build_c_multi_device()
+    p = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "multi_device_c ok" in p.stdout, p.stdout + p.stderr
+    print(p.stdout.strip())
