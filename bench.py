@@ -4,15 +4,19 @@
 One "step" = one nexrReduceCopy launch over one batch: the BASELINE configs[1] workload, fp32 sum,
 K=2 inputs, M=1 output, 256 MiB per buffer, inputs already resident in HBM (synthetic uniform
 [-1, 1) data). Buffers rotate over 3 sets (2.3 GiB) so no step re-reads the previous step's
-Infinity-Cache-resident bytes. With N GPUs every rank runs its own independent 256 MiB chunk
-(configs[4]: no data-path collective; the barrier and the max-over-ranks timer are harness only),
-so value = N x bytes per step / max-over-ranks time (weak scaling).
+Infinity-Cache-resident bytes. With N GPUs every GPU runs its own independent 256 MiB chunk
+(configs[4], C5: no data-path collective and no RCCL), so value = N x bytes per step / max time
+(weak scaling). Two ways to drive N GPUs, both measuring the same thing:
 
-    python bench.py                       # N=1, default steps
-    torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+    python bench.py                                    # N=1 (+ C3/C4 extra configs, CPU baseline)
+    torchrun --nproc-per-node N bench.py --gpus N      # one process per GPU; gloo (CPU) barrier/max
+    python bench.py --gpus N                           # one process: nexrReduceCopyMultiDevice,
+                                                       #   a host thread + stream per GPU
+Either N > 1 way also times an N=1 leg on GPU 0 in the same run, and every GPU alone, and reports
+them beside the aggregate under `c5`.
 
 Prints ONE JSON line on rank 0 (keys per the driver contract, plus `roofline`, `cpu_baseline`,
-`h2d_inclusive`).
+`h2d_inclusive`, `extra_configs` at N=1 and `per_gpu` / `c5` at N>1).
 """
 from __future__ import annotations
 
@@ -28,6 +32,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+REF_CPU_GBS_SURVEY = 1.79  # the compiled reference reduceCopy, fp32 sum K=2, 1 core
 
 # datatype / op ids = ncclDataType_t / ncclDevRedOp_t
 CONFIGS = {
@@ -50,8 +55,12 @@ CONFIGS = {
     "c4_i8_prod": dict(workload="int8 prod, 4-input reduce-copy, 64 MiB per buffer", dt=0, dtype="int8", op=1,
                        arg=0, k=4, m=1, buf_bytes=64 << 20),
 }
+EXTRA_ORDER = ["c3_f16", "c3_bf16", "c4_i32_min", "c4_i32_max", "c4_i32_prod", "c4_i8_min", "c4_i8_max",
+               "c4_i8_prod"]
 ESZ = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2}
 METRIC = "device-resident reduce-copy GB/s, fp32 sum, K-way fan-in, 1/2/4/8 MI355X"
+KERNEL = "nexr::reduce_copy_kernel"
+DATA = "synthetic (uniform [-1,1) generated on device; inputs resident in HBM)"
 
 
 def algorithmic_bytes(cfg) -> int:
@@ -59,7 +68,7 @@ def algorithmic_bytes(cfg) -> int:
     return (cfg["k"] + cfg["m"]) * cfg["buf_bytes"]
 
 
-# ---- distributed plumbing (harness only: no data-path collective) -----------------------------
+# ---- harness plumbing (no data-path collective) ------------------------------------------------
 def local_device_index() -> int:
     """This rank's GPU: LOCAL_RANK, folded onto the visible devices (a launcher that gives every rank
     one visible GPU, or a rehearsal with more ranks than GPUs, still lands on a valid device)."""
@@ -68,10 +77,14 @@ def local_device_index() -> int:
 
 
 class Dist:
-    def __init__(self, backend: str | None):
+    """Barrier, max and gather over the ranks of a torchrun launch. The default backend is gloo: the
+    harness needs only host-side synchronisation (each rank synchronises its own GPU first), so the
+    multi-GPU line never depends on RCCL (north_star: no RCCL on this path). NEXR_BENCH_BACKEND=nccl
+    selects RCCL for the harness collectives instead."""
+
+    def __init__(self, backend: str | None = "gloo"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = local_device_index() if backend == "nccl" else int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
         self.backend = backend
         if self.world > 1:
@@ -80,7 +93,7 @@ class Dist:
             kw = {}
             if backend == "nccl":
                 import torch
-                kw["device_id"] = torch.device("cuda", self.local_rank)
+                kw["device_id"] = torch.device("cuda", local_device_index())
             dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world, **kw)
             self.pg = dist
 
@@ -88,11 +101,14 @@ class Dist:
         if self.pg:
             self.pg.barrier()
 
+    def _dev(self, device):
+        return device if self.backend == "nccl" else None
+
     def max(self, value: float, device=None) -> float:
         if not self.pg:
             return value
         import torch
-        t = torch.tensor([value], dtype=torch.float64, device=device if self.backend == "nccl" else None)
+        t = torch.tensor([value], dtype=torch.float64, device=self._dev(device))
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
@@ -101,8 +117,7 @@ class Dist:
         if not self.pg:
             return [list(values)]
         import torch
-        dev = device if self.backend == "nccl" else None
-        t = torch.tensor(values, dtype=torch.float64, device=dev)
+        t = torch.tensor(values, dtype=torch.float64, device=self._dev(device))
         out = [torch.empty_like(t) for _ in range(self.world)]
         self.pg.all_gather(out, t)
         return [o.tolist() for o in out]
@@ -112,7 +127,18 @@ class Dist:
             self.pg.destroy_process_group()
 
 
-def timed_steps(step, steps: int, warmup: int, sync, dist: Dist, device=None):
+class _Solo:
+    """A one-rank stand-in for Dist (the N=1 legs and the extra configs)."""
+    world, rank = 1, 0
+
+    def barrier(self):
+        pass
+
+    def max(self, value, device=None):
+        return value
+
+
+def timed_steps(step, steps: int, warmup: int, sync, dist, device=None):
     """W untimed steps, then EXACTLY `steps` steps bracketed by barrier + sync on both sides.
     Returns (local seconds, max-over-ranks seconds)."""
     for i in range(warmup):
@@ -130,13 +156,126 @@ def timed_steps(step, steps: int, warmup: int, sync, dist: Dist, device=None):
     return local, dist.max(local, device)
 
 
-# ---- CPU baseline: the oracle (C restatement) on a bounded sample ------------------------------
-def cpu_baseline(cfg, seconds: float = 10.0, threads: int = 1):
-    import numpy as np
-    import oracle
+# ---- one configuration on one GPU --------------------------------------------------------------
+class DeviceWorkload:
+    """R rotating buffer sets of one configuration on one GPU, and the timed launch loop over them."""
 
-    n = (32 << 20) // ESZ[cfg["dt"]]  # 32 MiB per buffer sample
-    rng = np.random.default_rng(7)
+    def __init__(self, pkg, cfg, device_index: int, seed: int, sets: int = 3):
+        import torch
+        self.pkg, self.cfg = pkg, cfg
+        self.dev = torch.device("cuda", device_index)
+        self.n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(seed)
+        self.sets = []
+        with torch.cuda.device(self.dev):
+            for _ in range(sets):
+                if cfg["dt"] in (6, 7, 9):
+                    tdt = {6: torch.float16, 7: torch.float32, 9: torch.bfloat16}[cfg["dt"]]
+                    srcs = [(torch.rand(self.n, device=self.dev, generator=g) * 2 - 1).to(tdt)
+                            for _ in range(cfg["k"])]
+                else:
+                    srcs = [torch.randint(0, 256, (cfg["buf_bytes"],), dtype=torch.uint8, device=self.dev,
+                                          generator=g) for _ in range(cfg["k"])]
+                dsts = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8, device=self.dev) for _ in range(cfg["m"])]
+                self.sets.append(([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts], srcs, dsts))
+            self.stream = torch.cuda.current_stream(self.dev)
+        self.handle = self.stream.cuda_stream
+
+    def work(self, i: int = 0):
+        sp, dp, _, _ = self.sets[i % len(self.sets)]
+        return self.pkg.make_work(sp, dp, self.n, self.cfg["arg"])
+
+    def run(self, steps: int, warmup: int, dist, per_launch: bool = False):
+        """Returns (local wall s, max-over-ranks wall s, average kernel s from HIP events recorded on
+        the launch stream around the timed region, or around every launch)."""
+        import torch
+        cfg, total = self.cfg, warmup + steps
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(total)]
+
+        def step(i):
+            sp, dp, _, _ = self.sets[i % len(self.sets)]
+            if per_launch or i == warmup:
+                ev[i][0].record(self.stream)
+            self.pkg.reduce_copy_ptrs(sp, dp, self.n, cfg["dt"], cfg["op"], cfg["arg"], None, False, self.handle)
+            if per_launch or i == total - 1:
+                ev[i][1].record(self.stream)
+
+        with torch.cuda.device(self.dev):
+            local_s, max_s = timed_steps(step, steps, warmup, lambda: torch.cuda.synchronize(self.dev), dist,
+                                         self.dev)
+        if per_launch:
+            ms = [ev[warmup + i][0].elapsed_time(ev[warmup + i][1]) for i in range(steps)]
+            kernel_s = sum(ms) / len(ms) / 1e3
+        else:
+            kernel_s = ev[warmup][0].elapsed_time(ev[total - 1][1]) / steps / 1e3
+        return local_s, max_s, kernel_s
+
+    def free(self):
+        import torch
+        self.sets = []
+        torch.cuda.empty_cache()
+
+
+def roofline(cfg, config_name: str, kernel_s: float, per_launch: bool = False) -> dict:
+    achieved = algorithmic_bytes(cfg) / kernel_s / 1e9
+    traffic, src = load_traffic(config_name)
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": KERNEL,
+            "avg_kernel_us": round(kernel_s * 1e6, 2),
+            "timing": ("HIP events around every launch on its stream" if per_launch else
+                       "HIP events around the timed region on the launch stream / steps"),
+            "traffic_source": src}
+
+
+def load_traffic(config_name: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config_name}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def extra_configs(pkg, steps: int = 20, warmup: int = 5, names=EXTRA_ORDER) -> dict:
+    """BASELINE configs[2] and [3] (C3 fp16/bf16 K=8 256 MiB, C4 int32/int8 min/max/prod K=4 64 MiB)
+    after the headline's timed region, each on 3 rotating buffer sets: W untimed + S timed launches,
+    average kernel time from HIP events on the launch stream."""
+    out = {}
+    for i, name in enumerate(names):
+        cfg = CONFIGS[name]
+        wl = DeviceWorkload(pkg, cfg, local_device_index(), seed=2000 + i)
+        _, _, kernel_s = wl.run(steps, warmup, _Solo())
+        wl.free()
+        r = roofline(cfg, name, kernel_s)
+        out[name] = {"workload": cfg["workload"], "dtype": cfg["dtype"], "bytes_per_launch": algorithmic_bytes(cfg),
+                     "achieved": r["achieved"], "frac": r["frac"], "avg_kernel_us": r["avg_kernel_us"],
+                     "traffic": r["traffic"], "traffic_source": r["traffic_source"], "steps": steps,
+                     "warmup": warmup}
+    return out
+
+
+# ---- CPU baseline: the oracle (C restatement) on the benchmarked configuration ------------------
+def usable_cores() -> tuple:
+    """(threads to use, how that was decided): the CPUs this process may run on, capped by the
+    cgroup's CPU quota when one is set (a GPU box shows the whole machine's CPUs but grants a share)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, f"sched_getaffinity {aff} CPUs" + (f", cgroup cpu.max quota {quota} CPUs" if quota else "")
+
+
+def cpu_sample(cfg, n: int, seed: int = 7):
+    import numpy as np
+    rng = np.random.default_rng(seed)
     store = {0: np.uint8, 1: np.uint8, 2: np.uint32, 3: np.uint32, 4: np.uint64, 5: np.uint64, 6: np.uint16,
              7: np.float32, 8: np.float64, 9: np.uint16}[cfg["dt"]]
     if cfg["dt"] == 7:
@@ -144,6 +283,16 @@ def cpu_baseline(cfg, seconds: float = 10.0, threads: int = 1):
     else:
         srcs = [rng.integers(0, 256, n * ESZ[cfg["dt"]], dtype=np.uint8).view(store) for _ in range(cfg["k"])]
     dsts = [np.empty_like(srcs[0]) for _ in range(cfg["m"])]
+    return srcs, dsts
+
+
+def cpu_baseline(cfg, seconds: float = 10.0, threads: int = 1, sample=None):
+    """The C oracle over the FULL configuration (every buffer at cfg['buf_bytes']) for about
+    `seconds`: returns (GB/s of algorithmic bytes, calls, seconds)."""
+    import oracle
+
+    n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
+    srcs, dsts = sample if sample is not None else cpu_sample(cfg, n)
     oracle.reduce_copy(srcs, cfg["m"], cfg["dt"], cfg["op"], cfg["arg"], dsts=dsts, threads=threads)  # warm
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -152,7 +301,7 @@ def cpu_baseline(cfg, seconds: float = 10.0, threads: int = 1):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    gbs = reps * (cfg["k"] + cfg["m"]) * n * ESZ[cfg["dt"]] / el / 1e9
+    gbs = reps * algorithmic_bytes(cfg) / el / 1e9
     return gbs, reps, el
 
 
@@ -167,135 +316,35 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def load_traffic(config_name: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config_name}.json")
-    if not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+def cpu_baseline_entry(cfg, seconds: float) -> dict:
+    n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
+    sample = cpu_sample(cfg, n)
+    gbs1, reps1, el1 = cpu_baseline(cfg, seconds, threads=1, sample=sample)
+    nthreads, how = usable_cores()
+    gbsN, repsN, elN = cpu_baseline(cfg, max(2.0, seconds / 4), threads=nthreads, sample=sample)
+    mib = cfg["buf_bytes"] >> 20
+    return {"value": round(gbs1, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"the full benchmarked call: {cfg['k']} x {mib} MiB in, {cfg['m']} x {mib} MiB out "
+                      f"({cfg['workload']}), {reps1} calls in {el1:.1f} s on 1 thread of {cpu_model()}",
+            "note": "times oracle/nexr_oracle.c, the build's C restatement of reduceCopy (one thread = the "
+                    "reference emulator, which runs a launch's fibers on one pthread); the compiled reference "
+                    f"reduceCopy itself ran at {REF_CPU_GBS_SURVEY} GB/s on one core in the survey (SURVEY §6)",
+            "all_cores": {"value": round(gbsN, 3), "cores": nthreads, "cores_from": how,
+                          "sample": f"{repsN} calls in {elN:.1f} s, one pthread per contiguous slice"}}
 
 
-def main(argv=None):
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-h2d", action="store_true")
-    ap.add_argument("--no-xgmi", action="store_true", help="skip the xGMI peer-step probe (N > 1 only)")
-    ap.add_argument("--events", choices=["launch", "region"], default="region",
-                    help="HIP events around every launch (default) or only around the timed region")
-    args = ap.parse_args(argv)
-
-    import numpy as np
-    import torch
-
-    cfg = CONFIGS[args.config]
-    local_rank = local_device_index()
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    # NEXR_BENCH_BACKEND=gloo: rehearse the N > 1 harness where RCCL cannot run (several ranks on one
-    # GPU); the barrier and max-over-ranks timer are the only collectives either way.
-    dist = Dist(os.environ.get("NEXR_BENCH_BACKEND", "nccl"))
-    if dist.world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={dist.world}")
-    pkg = importlib.import_module("nex-nccl_amd")
-    pkg.lib()
-
-    esz = ESZ[cfg["dt"]]
-    n = cfg["buf_bytes"] // esz
-    R = 3
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + dist.rank)
-    sets = []
-    for r in range(R):
-        if cfg["dt"] in (6, 7, 9):
-            tdt = {6: torch.float16, 7: torch.float32, 9: torch.bfloat16}[cfg["dt"]]
-            srcs = [(torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt) for _ in range(cfg["k"])]
-        else:
-            srcs = [torch.randint(0, 256, (cfg["buf_bytes"],), dtype=torch.uint8, device=dev, generator=g)
-                    for _ in range(cfg["k"])]
-        dsts = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8, device=dev) for _ in range(cfg["m"])]
-        sets.append(([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts], srcs, dsts))
-    stream = torch.cuda.current_stream(dev)
-    handle = stream.cuda_stream
-    total = args.warmup + args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(total)]
-
-    per_launch = args.events == "launch"
-
-    def step(i):
-        sp, dp, _, _ = sets[i % R]
-        if per_launch or i == args.warmup:
-            ev[i][0].record(stream)
-        pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, handle)
-        if per_launch or i == total - 1:
-            ev[i][1].record(stream)
-
-    local_s, max_s = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, dist, dev)
-    if per_launch:
-        kernel_ms = [ev[args.warmup + i][0].elapsed_time(ev[args.warmup + i][1]) for i in range(args.steps)]
-        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    else:
-        avg_kernel_s = ev[args.warmup][0].elapsed_time(ev[total - 1][1]) / args.steps / 1e3
-    bytes_step = algorithmic_bytes(cfg)
-    value = dist.world * bytes_step * args.steps / max_s / 1e9
-    achieved = bytes_step / avg_kernel_s / 1e9
-    traffic, traffic_src = load_traffic(args.config)
-    # SURVEY §8(d) C5: per-GPU rates beside the aggregate (every rank's own wall time and kernel time).
-    ranks = dist.gather([local_s, avg_kernel_s], dev)
-
-    result = None
-    if dist.rank == 0:
-        cpu = None
-        h2d = None
-        if dist.world == 1 and not args.no_cpu:
-            gbs1, reps, el = cpu_baseline(cfg, args.cpu_seconds, threads=1)
-            nthreads = min(16, os.cpu_count() or 1)
-            gbsN, _, _ = cpu_baseline(cfg, max(2.0, args.cpu_seconds / 4), threads=nthreads)
-            cpu = {"value": round(gbs1, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle/nexr_oracle.c (C restatement of reduceCopy), same op/dtype/K/M, "
-                             f"32 MiB per buffer x {reps} reps in {el:.1f} s on 1 thread of {cpu_model()}",
-                   "all_cores": {"value": round(gbsN, 3), "cores": nthreads}}
-        if dist.world == 1 and not args.no_h2d:
-            h2d = h2d_inclusive(pkg, cfg, n)
-        xgmi = xgmi_probe() if dist.world > 1 and not args.no_xgmi else None
-        result = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GB/s",
-            "n_gpus": dist.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(max_s / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": cfg["dtype"],
-            "data": "synthetic (uniform [-1,1) generated on device; inputs resident in HBM)",
-            "config": {"workload": cfg["workload"], "k_inputs": cfg["k"], "m_outputs": cfg["m"],
-                       "bytes_per_buffer": cfg["buf_bytes"], "bytes_per_step_per_gpu": bytes_step,
-                       "parallelism": f"independent chunks x{dist.world} (no collective)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                         "kernel": "nexr::reduce_copy_kernel", "avg_kernel_us": round(avg_kernel_s * 1e6, 2),
-                         "timing": ("HIP events around every launch on its stream" if per_launch else
-                                    "HIP events around the timed region on the launch stream / steps"),
-                         "traffic_source": traffic_src},
-            "cpu_baseline": cpu,
-            "h2d_inclusive": h2d,
-        }
-        if dist.world > 1:
-            result["per_gpu"] = per_gpu_summary(ranks, bytes_step, args.steps)
-        if xgmi is not None:
-            result["xgmi_probe"] = xgmi
-        print(json.dumps(result), flush=True)
-    dist.close()
-    return result
+# ---- N > 1: the C5 summary ----------------------------------------------------------------------
+def c5_summary(n_gpus: int, bytes_step: int, steps: int, agg_seconds: float, n1_seconds: float,
+               solo_seconds: list) -> dict:
+    """aggregate GB/s over all GPUs, the same-run N=1 leg on GPU 0, every GPU's own
+    rate when it runs alone, and aggregate / (N x N=1) as measured in this run."""
+    agg = n_gpus * bytes_step * steps / agg_seconds / 1e9
+    n1 = bytes_step * steps / n1_seconds / 1e9
+    solo = [bytes_step * steps / s / 1e9 for s in solo_seconds]
+    return {"aggregate_gbs": round(agg, 2), "n1_same_run_gbs": round(n1, 2),
+            "solo_gbs_per_gpu": [round(x, 1) for x in solo],
+            "aggregate_over_n_times_n1": round(agg / (n_gpus * n1), 4),
+            "note": "per-GPU chunks are independent (no collective); solo_gbs_per_gpu = each GPU timed alone"}
 
 
 def per_gpu_summary(ranks, bytes_step: int, steps: int) -> dict:
@@ -308,7 +357,27 @@ def per_gpu_summary(ranks, bytes_step: int, steps: int) -> dict:
             "min_wall_gbs": round(min(wall), 2), "max_wall_gbs": round(max(wall), 2)}
 
 
-def xgmi_probe(timeout_s: float = 150.0):
+def base_line(cfg, n_gpus: int, steps: int, warmup: int, value: float, max_s: float, parallelism: str) -> dict:
+    return {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": n_gpus,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(max_s / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": cfg["dtype"],
+        "data": DATA,
+        "config": {"workload": cfg["workload"], "k_inputs": cfg["k"], "m_outputs": cfg["m"],
+                   "bytes_per_buffer": cfg["buf_bytes"], "bytes_per_step_per_gpu": algorithmic_bytes(cfg),
+                   "parallelism": parallelism},
+    }
+
+
+def xgmi_probe(timeout_s: float = 120.0):
     """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, in a bounded
     subprocess: its outcome is reported, never allowed to fail the bench line."""
     import subprocess
@@ -323,13 +392,15 @@ def xgmi_probe(timeout_s: float = 150.0):
         return {"error": repr(e)[:300]}
 
 
-def h2d_inclusive(pkg, cfg, n, reps: int = 3):
+def h2d_inclusive(pkg, cfg, reps: int = 3):
     """Rate with the host<->device traffic included (nexrReduceCopyHost on host buffers).
 
     Pinned buffers take the zero-copy path (the kernel reads/writes host memory over PCIe, both
     directions at once); pageable buffers take the staged two-stream chunk pipeline."""
     import numpy as np
     import torch
+
+    n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
 
     def run(srcs, dsts):
         sp = [s.data_ptr() if hasattr(s, "data_ptr") else s.ctypes.data for s in srcs]
@@ -355,6 +426,127 @@ def h2d_inclusive(pkg, cfg, n, reps: int = 3):
             "path": "nexrReduceCopyHost, pinned host buffers: zero-copy kernel over PCIe Gen5 x16",
             "pageable": {"value": round(alg / t_page / 1e9, 2), "ms_per_call": round(t_page * 1e3, 3),
                          "path": "staged H2D -> kernel -> D2H, two-stream 8 MiB chunk pipeline"}}
+
+
+# ---- the two ways to drive N GPUs ---------------------------------------------------------------
+def main_ranks(args, cfg, pkg) -> dict | None:
+    """One process per GPU (N=1 plain, or N>1 under torchrun): each rank times its own chunk."""
+    import torch
+
+    dist = Dist(os.environ.get("NEXR_BENCH_BACKEND", "gloo"))
+    if dist.world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={dist.world}")
+    dev_index = local_device_index()
+    torch.cuda.set_device(dev_index)
+    per_launch = args.events == "launch"
+    wl = DeviceWorkload(pkg, cfg, dev_index, seed=1000 + dist.rank)
+    local_s, max_s, kernel_s = wl.run(args.steps, args.warmup, dist, per_launch)
+    bytes_step = algorithmic_bytes(cfg)
+    value = dist.world * bytes_step * args.steps / max_s / 1e9
+    ranks = dist.gather([local_s, kernel_s], wl.dev)
+    c5 = None
+    if dist.world > 1:
+        # Same-run legs: rank 0's GPU alone (the N=1 reference), then every GPU alone in turn.
+        solo = []
+        for r in range(dist.world):
+            dist.barrier()
+            s = wl.run(args.steps, args.warmup, _Solo())[0] if dist.rank == r else 0.0
+            solo.append(dist.max(s, wl.dev))
+            dist.barrier()
+        c5 = c5_summary(dist.world, bytes_step, args.steps, max_s, solo[0], solo)
+    result = None
+    if dist.rank == 0:
+        result = base_line(cfg, dist.world, args.steps, args.warmup, value, max_s,
+                           f"independent chunks x{dist.world} (no collective)" +
+                           (f", one process per GPU ({dist.backend} barrier)" if dist.world > 1 else ""))
+        result["roofline"] = roofline(cfg, args.config, kernel_s, per_launch)
+        result["cpu_baseline"] = None
+        result["h2d_inclusive"] = None
+        if dist.world == 1:
+            if not args.no_extra:
+                wl.free()
+                result["extra_configs"] = extra_configs(pkg)
+            if not args.no_cpu:
+                result["cpu_baseline"] = cpu_baseline_entry(cfg, args.cpu_seconds)
+            if not args.no_h2d:
+                result["h2d_inclusive"] = h2d_inclusive(pkg, cfg)
+        else:
+            result["per_gpu"] = per_gpu_summary(ranks, bytes_step, args.steps)
+            result["c5"] = c5
+            if not args.no_xgmi:
+                result["xgmi_probe"] = xgmi_probe()
+        print(json.dumps(result), flush=True)
+    dist.barrier()
+    dist.close()
+    return result
+
+
+def main_fanout(args, cfg, pkg) -> dict:
+    """N>1 GPUs from ONE process, no launcher: nexrReduceCopyMultiDevice runs GPU d's chunk on a host
+    thread of its own (hipSetDevice, its own stream, a shared start barrier, hipStreamSynchronize).
+    The library reports the time from the barrier's release to the last GPU's completion."""
+    import torch
+
+    n_vis = torch.cuda.device_count()
+    if n_vis < args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but only {n_vis} visible GPU(s)")
+    wls = [DeviceWorkload(pkg, cfg, d, seed=1000 + d, sets=1) for d in range(args.gpus)]
+    for d in range(args.gpus):
+        torch.cuda.synchronize(d)
+    works = [wl.work(0) for wl in wls]
+    devices = list(range(args.gpus))
+    bytes_step = algorithmic_bytes(cfg)
+
+    def timed(ws, ds):
+        pkg.reduce_copy_multi_device(ws, ds, cfg["dt"], cfg["op"], reps=max(1, args.warmup))
+        return pkg.reduce_copy_multi_device(ws, ds, cfg["dt"], cfg["op"], reps=args.steps)
+
+    agg_s = timed(works, devices)
+    solo = [timed([works[d]], [d]) for d in devices]
+    value = args.gpus * bytes_step * args.steps / agg_s / 1e9
+    result = base_line(cfg, args.gpus, args.steps, args.warmup, value, agg_s,
+                       f"independent chunks x{args.gpus} (no collective), one process, "
+                       f"nexrReduceCopyMultiDevice (a host thread + stream per GPU)")
+    # Roofline of the kernel itself: HIP events on GPU 0's launch stream, 3 rotating sets.
+    for wl in wls:
+        wl.free()
+    wl0 = DeviceWorkload(pkg, cfg, 0, seed=1000)
+    _, _, kernel_s = wl0.run(args.steps, args.warmup, _Solo())
+    wl0.free()
+    result["roofline"] = roofline(cfg, args.config, kernel_s)
+    result["cpu_baseline"] = None
+    result["h2d_inclusive"] = None
+    result["c5"] = c5_summary(args.gpus, bytes_step, args.steps, agg_s, solo[0], solo)
+    result["c5"]["timing"] = "nexrReduceCopyMultiDevice: barrier release to the last GPU's completion"
+    if not args.no_xgmi:
+        result["xgmi_probe"] = xgmi_probe()
+    print(json.dumps(result), flush=True)
+    return result
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-h2d", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3/C4 extra configurations (N=1 only)")
+    ap.add_argument("--no-xgmi", action="store_true", help="skip the xGMI peer-step probe (N > 1 only)")
+    ap.add_argument("--events", choices=["launch", "region"], default="region",
+                    help="HIP events around every launch, or only around the timed region (default)")
+    args = ap.parse_args(argv)
+    if args.config != "c2":
+        args.no_extra = True  # the extras are measured beside the headline configuration only
+
+    pkg = importlib.import_module("nex-nccl_amd")
+    pkg.lib()
+    cfg = CONFIGS[args.config]
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        return main_fanout(args, cfg, pkg)
+    return main_ranks(args, cfg, pkg)
 
 
 if __name__ == "__main__":

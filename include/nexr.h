@@ -23,6 +23,9 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -83,11 +86,14 @@ typedef enum {
   nexrNumDevRedOps = 5
 } nexrDevRedOp_t;
 
-/* Mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693). */
+/* Byte-exact mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693):
+ * two 4-byte enums at offsets 0 and 4, a one-byte bool at offset 8 (bytes 9-15 are padding the
+ * library never reads), the 64-bit scalar at offset 16; sizeof == 24. tests/test_abi.py checks the
+ * layout against a C restatement of the reference struct. */
 typedef struct {
-  int op;              /* nexrDevRedOp_t */
-  int proxyOp;         /* nexrRedOp_t the user asked for */
-  int scalarArgIsPtr;  /* scalarArg holds a device pointer to the scalar (onerank.cc:32-42) */
+  int op;               /* nexrDevRedOp_t (ncclDevRedOp_t, an int-sized enum) */
+  int proxyOp;          /* nexrRedOp_t the user asked for */
+  bool scalarArgIsPtr;  /* scalarArg holds a device pointer to the scalar (onerank.cc:32-42) */
   uint64_t scalarArg;
 } nexrDevRedOpFull;
 
@@ -242,6 +248,31 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
                                           const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
                                           uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
                                           nexrStream_t stream);
+
+/*
+ * nexrQueryLaunch — diagnostics: the launch nexrReduceCopy would make for these pointers and this
+ * size (no GPU work, no device needed; the same validation as nexrReduceCopy with devRedOp = Sum).
+ * `generic` is 1 when the pointers share no 16-B phase and every element takes the scalar path;
+ * otherwise [0, headElts) and the tail are edge elements and bodyPacks 16-B packs form the aligned
+ * body. grid * block never exceeds 2^32 - 1 work items (HIP's launch limit); larger calls
+ * grid-stride. policy: 0 plain, 1 non-temporal loads, 3 non-temporal loads and stores.
+ */
+typedef struct {
+  uint32_t grid;
+  int block;
+  int packsPerLane;
+  int policy;
+  int generic;
+  uint64_t headElts;
+  uint64_t bodyPacks;
+} nexrLaunchInfo;
+NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                      size_t nElts, int datatype, nexrLaunchInfo* info);
+
+/* Diagnostics: how many streams nexrReduceCopyMultiDevice and how many staging rings
+ * nexrReduceCopyHost have created in this process so far (both are pooled and reused, so the counts
+ * stop growing once the pools are warm). Either pointer may be NULL. */
+NEXR_API nexrResult_t nexrGetPoolStats(uint64_t* multiDeviceStreams, uint64_t* hostStagingRings);
 
 /* Bytes per element of a datatype (reference ncclTypeSize), 0 if unknown. */
 NEXR_API size_t nexrTypeSize(int datatype);

@@ -77,7 +77,8 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
 
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
-               "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion", "nexrGetLastHipError")
+               "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrQueryLaunch", "nexrGetPoolStats", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion",
+               "nexrGetLastHipError")
 
 
 class NexrError(RuntimeError):
@@ -91,9 +92,17 @@ class NexrError(RuntimeError):
 
 
 class DevRedOpFull(ctypes.Structure):
-    """Mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693)."""
-    _fields_ = [("op", ctypes.c_int), ("proxyOp", ctypes.c_int), ("scalarArgIsPtr", ctypes.c_int),
+    """Byte-exact mirror of struct ncclDevRedOpFull (reference src/include/device.h:688-693): enum op
+    at 0, enum proxyOp at 4, bool scalarArgIsPtr at 8 (9-15 padding), uint64 scalarArg at 16."""
+    _fields_ = [("op", ctypes.c_int), ("proxyOp", ctypes.c_int), ("scalarArgIsPtr", ctypes.c_bool),
                 ("scalarArg", ctypes.c_uint64)]
+
+
+class LaunchInfo(ctypes.Structure):
+    """Mirror of nexrLaunchInfo (include/nexr.h): what nexrQueryLaunch reports."""
+    _fields_ = [("grid", ctypes.c_uint32), ("block", ctypes.c_int), ("packsPerLane", ctypes.c_int),
+                ("policy", ctypes.c_int), ("generic", ctypes.c_int), ("headElts", ctypes.c_uint64),
+                ("bodyPacks", ctypes.c_uint64)]
 
 
 MAX_BATCH_WORKS = 14  # NEXR_MAX_BATCH_WORKS
@@ -132,6 +141,10 @@ def lib() -> ctypes.CDLL:
     L.nexrHostToDevRedOp.restype = i32
     L.nexrLaunchOneRank.argtypes = [vp, vp, sz, DevRedOpFull, i32, vp]
     L.nexrLaunchOneRank.restype = i32
+    L.nexrQueryLaunch.argtypes = [i32, P(vp), i32, P(vp), sz, i32, P(LaunchInfo)]
+    L.nexrQueryLaunch.restype = i32
+    L.nexrGetPoolStats.argtypes = [P(u64), P(u64)]
+    L.nexrGetPoolStats.restype = i32
     L.nexrReduceCopyLL.argtypes = [vp, i32, i32, P(vp), P(ctypes.c_uint32), vp, i32, P(vp), P(ctypes.c_uint32), sz,
                                    i32, i32, u64, i32, vp, ctypes.c_uint32, vp]
     L.nexrReduceCopyLL.restype = i32
@@ -231,6 +244,22 @@ def reduce_copy_multi_device(works: Sequence[ReduceCopyWork], devices: Sequence[
     _check(lib().nexrReduceCopyMultiDevice(arr, dev, len(works), int(datatype), int(dev_red_op), int(reps),
                                            ctypes.byref(secs)), "nexrReduceCopyMultiDevice")
     return secs.value
+
+
+def query_launch(srcs: Sequence[int], dsts: Sequence[int], n_elts: int, datatype: int) -> LaunchInfo:
+    """nexrQueryLaunch: the grid, block, cache policy and edge/body split nexrReduceCopy would use
+    (no device work)."""
+    info = LaunchInfo()
+    _check(lib().nexrQueryLaunch(len(srcs), _ptr_array(srcs), len(dsts), _ptr_array(dsts), int(n_elts),
+                                 int(datatype), ctypes.byref(info)), "nexrQueryLaunch")
+    return info
+
+
+def pool_stats() -> tuple:
+    """(streams created by nexrReduceCopyMultiDevice, staging rings created by nexrReduceCopyHost)."""
+    a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(lib().nexrGetPoolStats(ctypes.byref(a), ctypes.byref(b)), "nexrGetPoolStats")
+    return a.value, b.value
 
 
 def host_to_dev_red_op(op: int, datatype: int, n_ranks: int = 1) -> DevRedOpFull:

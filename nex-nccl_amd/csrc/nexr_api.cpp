@@ -46,18 +46,21 @@ long envLong(const char* name, long dflt) {
   return strtol(v, nullptr, 0);
 }
 
-// Grid: one workgroup per kTripPacks-pack trip ("one-shot"), capped at 2^24 workgroups beyond
-// which the kernel grid-strides. Policy by the bytes the call streams (every src read once, every
+// Grid: one workgroup per kTripPacks-pack trip ("one-shot"), capped so that grid x block stays
+// within HIP's 2^32 - 1 work-item limit (2^24 workgroups of 256 lanes, 2^22 of 1024); beyond the
+// cap the kernel grid-strides. Policy by the bytes the call streams (every src read once, every
 // dst written once): plain below NEXR_NT_LOAD_MIN_BYTES (64 MiB: the data likely sits in L2/MALL
 // and the consumer wants the output there too), non-temporal loads above it, non-temporal loads
 // and stores above NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3)
 // and NEXR_GRID override for sweeps.
-nexrResult_t pickGeometry(uint64_t workgroups, uint64_t streamBytes, Geometry* g) {
+uint64_t gridCap(int block) { return 0xffffffffull / (uint64_t)block; }
+
+nexrResult_t pickGeometry(uint64_t workgroups, uint64_t streamBytes, int block, Geometry* g) {
   static const long gridOverride = envLong("NEXR_GRID", 0);
   static const long polOverride = envLong("NEXR_POLICY", -1);
   static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);
   static const long ntStoreMin = envLong("NEXR_NT_STORE_MIN_BYTES", 512l << 20);
-  const uint64_t cap = 1ull << 24;
+  const uint64_t cap = gridCap(block);
   uint64_t need = workgroups < 1 ? 1 : workgroups;
   g->grid = (int)(need < cap ? need : cap);
   if (gridOverride > 0) g->grid = (int)gridOverride;
@@ -171,7 +174,7 @@ hipError_t launchBatchDt(int dt, const BatchParams& b, int op, int nSrcs, int po
 }
 
 // One batch launch per (nSrcs, run of <= kMaxBatch works): work i gets
-// max(1, workgroupsFor(work i)) workgroups (its one-shot grid), total capped at 2^24 by
+// max(1, workgroupsFor(work i)) workgroups (its one-shot grid), total capped at gridCap(block) by
 // shrinking the largest shares (the kernel grid-strides inside each work's range).
 nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int op, hipStream_t stream) {
   if (nWorks < 0 || (nWorks > 0 && works == nullptr)) return nexrInvalidArgument;
@@ -182,8 +185,8 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
     if (r != nexrSuccess) return r;
   }
   const size_t esz = typeSize(datatype);
-  const uint64_t cap = 1ull << 24;
   for (int k = 1; k <= NEXR_MAX_SRCS; k++) {
+    const uint64_t cap = gridCap(block_for(datatype, k));
     BatchParams b;
     b.nWorks = 0;
     uint64_t blocks[kMaxBatch];
@@ -203,7 +206,7 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
       b.start[0] = 0;
       for (int i = 0; i < b.nWorks; i++) b.start[i + 1] = b.start[i] + (uint32_t)blocks[i];
       Geometry g;
-      nexrResult_t r = pickGeometry(total, streamBytes, &g);
+      nexrResult_t r = pickGeometry(total, streamBytes, block_for(datatype, k), &g);
       if (r != nexrSuccess) return r;
       NEXR_HIP(launchBatchDt(datatype, b, op, k, g.pol, (int)total, stream));
       b.nWorks = 0;
@@ -240,7 +243,8 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   RCParams p;
   fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, nPreOpSrcs, preOpArgs, prePtr, postOp);
   Geometry g;
-  r = pickGeometry(workgroupsFor(p, nSrcs, datatype), (uint64_t)(nSrcs + nDsts) * nElts * esz, &g);
+  r = pickGeometry(workgroupsFor(p, nSrcs, datatype), (uint64_t)(nSrcs + nDsts) * nElts * esz,
+                   block_for(datatype, nSrcs), &g);
   if (r != nexrSuccess) return r;
   NEXR_HIP(launchDt(datatype, p, op, nSrcs, g, stream));
   return nexrSuccess;
@@ -255,6 +259,7 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
 // dominated calls of tens of MiB; profiles/r01s5_c_examples_gpu.txt.)
 std::mutex gMdStreamMu;
 std::vector<std::pair<int, hipStream_t>> gMdStreamIdle;
+uint64_t gMdStreamsCreated = 0;  // under gMdStreamMu (nexrGetPoolStats)
 
 hipError_t mdStreamTake(int dev, hipStream_t* st) {
   {
@@ -266,7 +271,12 @@ hipError_t mdStreamTake(int dev, hipStream_t* st) {
         return hipSuccess;
       }
   }
-  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  hipError_t e = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> g(gMdStreamMu);
+    gMdStreamsCreated++;
+  }
+  return e;
 }
 
 void mdStreamGive(int dev, hipStream_t st) {  // st was synchronised without error
@@ -297,6 +307,7 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
   std::vector<std::chrono::steady_clock::time_point> t1(nWorks);
   std::vector<nexrResult_t> res(nWorks, nexrSuccess);
   std::vector<int> hipErr(nWorks, 0);
+  bool cancel = false;  // set (under mu) when not every work got a thread: nothing runs
   auto run = [&](int i) {
     const nexrReduceCopyWork& w = works[i];
     hipStream_t st = nullptr;
@@ -314,6 +325,7 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
       } else {
         cv.wait(lk, [&] { return arrived == nWorks; });
       }
+      if (cancel && res[i] == nexrSuccess) res[i] = nexrSystemError;
     }
     for (int k = 0; k < reps && res[i] == nexrSuccess; k++)
       res[i] = reduceCopyDevice(w.nSrcs, w.srcs, w.nDsts, w.dsts, w.nElts, datatype, op, w.redOpArg, w.nPreOpSrcs,
@@ -333,9 +345,23 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
     }
   };
   std::vector<std::thread> threads;
-  threads.reserve(nWorks);
-  for (int i = 0; i < nWorks; i++) threads.emplace_back(run, i);
+  bool spawnFailed = false;
+  try {
+    threads.reserve(nWorks);
+    for (int i = 0; i < nWorks; i++) threads.emplace_back(run, i);
+  } catch (...) {
+    // A thread could not be created: the works that never got one count as arrived (so the started
+    // threads leave the barrier), but none of them may run, and the call reports a system error.
+    std::lock_guard<std::mutex> lk(mu);
+    spawnFailed = true;
+    cancel = true;
+    for (int i = (int)threads.size(); i < nWorks; i++) res[i] = nexrSystemError;
+    arrived += nWorks - (int)threads.size();
+    if (arrived == nWorks) t0 = std::chrono::steady_clock::now();
+    cv.notify_all();
+  }
   for (auto& t : threads) t.join();
+  if (spawnFailed) return nexrSystemError;
   for (int i = 0; i < nWorks; i++)
     if (res[i] != nexrSuccess) {
       tLastHipError = hipErr[i];
@@ -366,6 +392,7 @@ struct HostStage {
 };
 std::mutex gStageMu;
 std::vector<HostStage*> gStageIdle;
+uint64_t gStagesCreated = 0;  // under gStageMu (nexrGetPoolStats)
 
 // Checks a ring out for the current device (the largest idle one, or a new one) and hands it back
 // when the call ends. Release drains the ring's stream and the caller's stream first, so that no
@@ -404,16 +431,23 @@ nexrResult_t stageFor(size_t slotBytes, hipStream_t caller, StageLease* lease) {
   }
   if (!st) {
     st = new HostStage();
-    if (hipStreamCreateWithFlags(&st->out, hipStreamNonBlocking) != hipSuccess) {
-      delete st;
-      return hipFail(hipGetLastError());
+    hipError_t e = hipStreamCreateWithFlags(&st->out, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) {
+      e = hipEventCreateWithFlags(&st->kernelDone[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&st->outDone[i], hipEventDisableTiming);
     }
-    for (int i = 0; i < 2; i++) {
-      if (hipEventCreateWithFlags(&st->kernelDone[i], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&st->outDone[i], hipEventDisableTiming) != hipSuccess)
-        return hipFail(hipGetLastError());  // the half-built ring is not pooled
+    if (e != hipSuccess) {  // free the half-built ring; it is never pooled
+      for (int i = 0; i < 2; i++) {
+        if (st->kernelDone[i]) (void)hipEventDestroy(st->kernelDone[i]);
+        if (st->outDone[i]) (void)hipEventDestroy(st->outDone[i]);
+      }
+      if (st->out) (void)hipStreamDestroy(st->out);
+      delete st;
+      return hipFail(e);
     }
     st->device = dev;
+    std::lock_guard<std::mutex> g(gStageMu);
+    gStagesCreated++;
   }
   lease->st = st;
   lease->caller = caller;
@@ -471,6 +505,42 @@ NEXR_API nexrResult_t nexrReduceCopy(int nSrcs, const void* const* srcs, int nDs
                                      nexrStream_t stream) {
   return reduceCopyDevice(nSrcs, srcs, nDsts, dsts, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs,
                           preOpArgs, nullptr, postOp, (hipStream_t)stream);
+}
+
+NEXR_API nexrResult_t nexrGetPoolStats(uint64_t* multiDeviceStreams, uint64_t* hostStagingRings) {
+  if (multiDeviceStreams) {
+    std::lock_guard<std::mutex> g(gMdStreamMu);
+    *multiDeviceStreams = gMdStreamsCreated;
+  }
+  if (hostStagingRings) {
+    std::lock_guard<std::mutex> g(gStageMu);
+    *hostStagingRings = gStagesCreated;
+  }
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
+                                      size_t nElts, int datatype, nexrLaunchInfo* info) {
+  if (info == nullptr) return nexrInvalidArgument;
+  memset(info, 0, sizeof(*info));
+  nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, nexrDevSum, 0, 0, nullptr);
+  if (r != nexrSuccess) return r;
+  if (nElts == 0 || nDsts == 0) return nexrSuccess;  // nothing would be launched
+  const size_t esz = typeSize(datatype);
+  RCParams p;
+  fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, 0, 0, nullptr, nullptr, 0);
+  Geometry g;
+  const int block = block_for(datatype, nSrcs);
+  r = pickGeometry(workgroupsFor(p, nSrcs, datatype), (uint64_t)(nSrcs + nDsts) * nElts * esz, block, &g);
+  if (r != nexrSuccess) return r;
+  info->grid = (uint32_t)g.grid;
+  info->block = block;
+  info->packsPerLane = p.generic ? 1 : unroll_for(datatype, nSrcs);
+  info->policy = g.pol;
+  info->generic = p.generic;
+  info->headElts = p.head;
+  info->bodyPacks = p.nPacks;
+  return nexrSuccess;
 }
 
 NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int devRedOp,
@@ -578,7 +648,7 @@ NEXR_API nexrResult_t nexrHostToDevRedOp(nexrDevRedOpFull* opFull, int op, int d
   if (nbits <= 0) return nexrInvalidArgument;
   const uint64_t allBits = ~(uint64_t)0 >> (64 - nbits);
   const uint64_t signBit = allBits ^ (allBits >> 1);
-  opFull->scalarArgIsPtr = 0;
+  opFull->scalarArgIsPtr = false;
   opFull->proxyOp = op;
   opFull->scalarArg = 0;
   switch (op) {

@@ -89,6 +89,7 @@ struct alignas(64) PeerHeader {
 };
 struct PeerSlot {
   hipIpcMemHandle_t fifoHandle;
+  std::atomic<uint32_t> claimed;  // set once by rank r when it joins; already set = stale segment
   alignas(64) ConnState conn;
 };
 // Links beyond the ring for PAT (r -> r +- 2^d) and P2P (any r -> q), one per ordered pair: the

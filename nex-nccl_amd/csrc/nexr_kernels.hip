@@ -7,7 +7,8 @@
 //   - one 16-B load per lane per source per pack (global_load_dwordx4), 64-lane waves,
 //     4 waves per workgroup; each workgroup owns one 16 KiB trip of every buffer (U = 4 packs
 //     per lane, "one-shot" grid of nPacks/(256*4) workgroups; a grid-stride loop only beyond
-//     2^24 workgroups), so every lane has 4*K independent loads in flight;
+//     (2^32-1)/block workgroups, HIP's work-item limit), so every lane has 4*K independent loads
+//     in flight;
 //   - all K source loads of a trip are issued before the first reduce step;
 //   - cache policy by working-set size: non-temporal loads once a call streams more than
 //     64 MiB, non-temporal loads AND stores beyond 512 MiB (2x the Infinity Cache) —

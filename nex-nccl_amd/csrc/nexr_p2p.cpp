@@ -69,7 +69,7 @@ void runP2pHalf(nexrRingComm* c, Shared* sh, int rank, bool send, int peer, cons
                 size_t bytes) {
   hipStream_t s = send ? c->streams[rank] : c->streams2[rank];
   if (s) (void)hipSetDevice(c->devices[rank]);
-  const nexrDevRedOpFull copy = {nexrDevSum, 0, 0, 0};
+  const nexrDevRedOpFull copy = {nexrDevSum, 0, false, 0};
   const bool ll = p2pUsesLL(c, bytes);
   Prims p = makePrims(c, sh, rank, sendbuff, recvbuff, 1, nexrInt8, copy, kGeomPipe, s,
                       send ? c->status[rank] : c->status2[rank]);

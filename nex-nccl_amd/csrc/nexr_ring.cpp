@@ -1031,6 +1031,14 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   };
   uint32_t fresh = 0;
   if (h->initState.compare_exchange_strong(fresh, 1)) {
+    // The first rank configures the segment; every slot, link and counter starts from zero even if
+    // the name was reused (the others touch nothing before initState == 2).
+    memset((char*)c->shm + sizeof(PeerHeader), 0, c->shmBytes - sizeof(PeerHeader));
+    h->joined.store(0);
+    h->left.store(0);
+    h->abort.store(0);
+    h->patJoined.store(0);
+    h->p2pJoined.store(0);
     h->magic = kPeerMagic;
     h->nRanks = (uint32_t)n;
     h->protocol = (uint32_t)c->proto;
@@ -1042,10 +1050,21 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   if (h->magic != kPeerMagic || h->nRanks != (uint32_t)n || h->protocol != (uint32_t)c->proto ||
       h->buffBytes != c->cfg.buffBytes)
     return fail(nexrInvalidUsage);  // ranks disagree on the communicator (or a stale segment)
+  // A segment left behind by an earlier communicator under the same name (a crashed run) still holds
+  // its ranks' claims and counters: joining it would inherit stale head/tail steps and handles, so it
+  // is refused. So is a second process claiming the same rank.
   PeerSlot* mine = peerSlot(c->shm, me);
+  uint32_t unclaimed = 0;
+  if (h->left.load(std::memory_order_acquire) != 0 || !mine->claimed.compare_exchange_strong(unclaimed, 1)) {
+    munmap(c->shm, c->shmBytes);  // not ours: leave its abort word and counters alone
+    c->shm = nullptr;
+    nexrRingCommDestroy(c);
+    return nexrInvalidUsage;
+  }
   if (hipIpcGetMemHandle(&mine->fifoHandle, c->conns[me]->fifo) != hipSuccess) return fail(nexrUnhandledCudaError);
   c->conns[me]->st = &mine->conn;
-  h->joined.fetch_add(1, std::memory_order_acq_rel);  // publishes the handle
+  if (h->joined.fetch_add(1, std::memory_order_acq_rel) >= (uint32_t)n)  // publishes the handle
+    return fail(nexrInvalidUsage);
   if (!waitFor([&] { return h->joined.load(std::memory_order_acquire) >= (uint32_t)n; })) return fail(nexrRemoteError);
   if (next != me) {
     hipIpcMemHandle_t hd = peerSlot(c->shm, next)->fifoHandle;

@@ -34,11 +34,19 @@ def main() -> int:
     n_in = a.count * a.n if a.coll in ("reducescatter", "pat_rs") else a.count
     n_out = a.count * a.n if a.coll in ("allgather", "pat_ag") else a.count
     inputs = mg.gen_inputs(a.dt, a.n, n_in, a.seed, special=True)
-    dev = torch.device("cuda:0")
+    # Rank r drives GPU r mod (visible GPUs): on a node every neighbour pair of the ring sits on two
+    # GPUs and each step's reduce-copy writes into the next rank's FIFO over xGMI; on a one-GPU box all
+    # ranks share GPU 0 and the same IPC mappings stay on the device.
+    ordinal = a.rank % torch.cuda.device_count()
+    torch.cuda.set_device(ordinal)
+    assert torch.cuda.current_device() == ordinal
+    dev = torch.device("cuda", ordinal)
+    with open(f"{a.out}.device", "w") as f:
+        f.write(f"{ordinal} {torch.cuda.device_count()}\n")
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
     recv = torch.zeros(n_out, dtype=send.dtype, device=dev)
     torch.cuda.synchronize()
-    with ring.PeerRingComm(a.n, a.rank, a.shm, device=0, buff_bytes=a.buff, protocol=a.proto,
+    with ring.PeerRingComm(a.n, a.rank, a.shm, device=ordinal, buff_bytes=a.buff, protocol=a.proto,
                            timeout_ms=60000) as comm:
         if a.coll != "allreduce":
             for call in range(a.calls):

@@ -90,6 +90,102 @@ def test_invalid_arguments_fail_before_the_device(nexr):
     assert L.nexrReduceCopy(2, sa, 1, da, 16, 7, 0, 0, 1, None, 0, None) == 4  # preOpArgs NULL
 
 
+# Restatement of the reference struct (src/include/device.h:682-693, src/nccl.h.in:259-270), compiled
+# beside include/nexr.h as C11 and as C++17 (the reference's host code is C++): the two layouts must be
+# identical, field by field.
+_REF_STRUCT = r"""
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+#include "nexr.h"
+typedef enum { ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg, ncclNumOps, ncclMaxRedOp = 0x7fffffff } ncclRedOp_t;
+enum ncclDevRedOp_t { ncclDevSum, ncclDevProd, ncclDevMinMax, ncclDevPreMulSum, ncclDevSumPostDiv, ncclNumDevRedOps };
+struct ncclDevRedOpFull {
+  enum ncclDevRedOp_t op;
+  ncclRedOp_t proxyOp;
+  bool scalarArgIsPtr;
+  uint64_t scalarArg;
+};
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(struct ncclDevRedOpFull), offsetof(struct ncclDevRedOpFull, op),
+         offsetof(struct ncclDevRedOpFull, proxyOp), offsetof(struct ncclDevRedOpFull, scalarArgIsPtr),
+         offsetof(struct ncclDevRedOpFull, scalarArg));
+  printf("%zu %zu %zu %zu %zu\n", sizeof(nexrDevRedOpFull), offsetof(nexrDevRedOpFull, op),
+         offsetof(nexrDevRedOpFull, proxyOp), offsetof(nexrDevRedOpFull, scalarArgIsPtr),
+         offsetof(nexrDevRedOpFull, scalarArg));
+  printf("%zu %zu\n", sizeof(((struct ncclDevRedOpFull*)0)->scalarArgIsPtr),
+         sizeof(((nexrDevRedOpFull*)0)->scalarArgIsPtr));
+  return 0;
+}
+"""
+
+
+@pytest.mark.parametrize("compiler,std,suffix", [("gcc", "-std=c11", ".c"), ("g++", "-std=c++17", ".cc")])
+def test_dev_red_op_full_is_byte_exact_with_reference(nexr, tmp_path, compiler, std, suffix):
+    src = tmp_path / ("layout" + suffix)
+    src.write_text(_REF_STRUCT)
+    exe = tmp_path / "layout"
+    subprocess.run([compiler, std, "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True, capture_output=True, text=True, timeout=120)
+    ref, ours, bools = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines()
+    assert ref == ours == "24 0 4 8 16"
+    assert bools == "1 1"
+    # The Python mirror has the same layout.
+    F = nexr.DevRedOpFull
+    assert ctypes.sizeof(F) == 24
+    assert (F.op.offset, F.proxyOp.offset, F.scalarArgIsPtr.offset, F.scalarArg.offset) == (0, 4, 8, 16)
+    assert F.scalarArgIsPtr.size == 1
+
+
+def test_dev_red_op_full_padding_is_never_read(nexr):
+    """A caller's struct whose padding bytes 9-15 are 0xFF still reads scalarArgIsPtr = false: the flag
+    is the single byte at offset 8 (with an int-sized flag, as in round 1, the same bytes read as a
+    non-zero int and the scalar would be dereferenced as a pointer)."""
+    raw = bytearray(24)
+    raw[0:4] = (3).to_bytes(4, "little")        # ncclDevPreMulSum
+    raw[4:8] = (0).to_bytes(4, "little")
+    raw[8] = 0
+    raw[9:16] = b"\xff" * 7
+    raw[16:24] = (0x3F800000).to_bytes(8, "little")
+    f = nexr.DevRedOpFull.from_buffer_copy(bytes(raw))
+    assert f.scalarArgIsPtr is False and f.op == 3 and f.scalarArg == 0x3F800000
+    # The C ABI receives exactly these 24 bytes by value (same layout as checked above).
+    assert bytes(f)[9:16] == b"\xff" * 7
+
+
+def test_query_launch_grid_respects_the_work_item_limit(nexr):
+    """Advisor r1: the grid cap must keep grid x block <= 2^32 - 1 (HIP's limit). A 2^32-element
+    generic-path call (pointers with mixed 16-B phases) needs ~2^32 work items; the launch must cap
+    the grid and grid-stride instead of failing."""
+    n = 1 << 32
+    # int8, K=2: mixed phases -> generic path, block 256
+    info = nexr.query_launch([0x1000, 0x2001], [0x3000], n, 0)
+    assert info.generic == 1 and info.block == 256
+    assert info.grid * info.block <= 0xFFFFFFFF
+    assert info.grid == 0xFFFFFFFF // 256
+    # fp16 K=8 (block 1024): a 16 GiB body would need 2^20 workgroups -> under the 2^22 cap
+    srcs = [0x10000 * (i + 1) for i in range(8)]
+    info = nexr.query_launch(srcs, [0x100000], 8 << 30, 6)
+    assert info.generic == 0 and info.block == 1024 and info.packsPerLane == 1
+    assert info.grid == (8 << 30) * 2 // 16 // 1024 and info.grid * info.block <= 0xFFFFFFFF
+    # generic fp16 K=8 at 2^33 elements: capped at (2^32-1) // 1024
+    info = nexr.query_launch([0x10000 * (i + 1) + (i & 1) * 2 for i in range(8)], [0x100000], 1 << 33, 6)
+    assert info.generic == 1 and info.grid == 0xFFFFFFFF // 1024
+    # C2 geometry: 256 MiB fp32 K=2, U=4 packs per lane, one 16 KiB trip per workgroup, nt loads
+    info = nexr.query_launch([0x10000000, 0x20000000], [0x30000000], 64 << 20, 7)
+    assert (info.grid, info.block, info.packsPerLane, info.policy) == (16384, 256, 4, 3)
+    # head/body/tail split for a shared 4-B phase
+    info = nexr.query_launch([0x1004, 0x2004], [0x3004], 100, 7)
+    assert (info.generic, info.headElts, info.bodyPacks) == (0, 3, 24)
+    # validation as nexrReduceCopy; empty calls launch nothing
+    with pytest.raises(nexr.NexrError):
+        nexr.query_launch([0x1000, 0], [0x3000], 16, 7)
+    assert nexr.query_launch([0x1000], [0x3000], 0, 7).grid == 0
+
+
 def test_empty_calls_are_noops(nexr):
     # nElts == 0 and nDsts == 0 return success without launching (common_kernel.h:288-289).
     assert _call(nexr, n=0) == 0
@@ -165,7 +261,7 @@ def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):
     else:
         exp = oracle.host_to_dev_red_op(op, dt, nranks)
     assert (out.op, out.scalarArg) == exp
-    assert out.proxyOp == op and out.scalarArgIsPtr == 0
+    assert out.proxyOp == op and out.scalarArgIsPtr is False
 
 
 def test_ring_library_exports_its_header():

@@ -211,18 +211,50 @@ def test_multi_device_concurrent_callers_share_the_stream_pool(nexr, dev):
         except Exception as e:  # noqa: BLE001 - reported below
             errors.append(repr(e))
 
+    created0, _ = nexr.pool_stats()
     threads = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
     [th.start() for th in threads]
     [th.join(timeout=60) for th in threads]
+    assert not any(th.is_alive() for th in threads), "a caller thread hung (stream sharing or deadlock)"
     assert not errors, errors
     for per in bufs:
         for a, b, o, d in per:
             with torch.cuda.device(d):
                 assert torch.equal(o, a + b)
-    # warm pool: the same calls again, one thread after another, each well under a fresh stream's
-    # ~1.5 ms first-launch cost (8 MiB of traffic per work and rep)
+    # The pool is bounded by the peak number of concurrent works (4 callers x 2 works), not by the
+    # number of calls (4 x 6 calls x 2 works = 48).
+    created1, _ = nexr.pool_stats()
+    assert created1 - created0 <= 8, (created0, created1)
+    # Warm pool: the same calls again, one thread after another, create no stream at all.
     for t in range(4):
         per = bufs[t]
         works = [nexr.make_work([a.data_ptr(), b.data_ptr()], [o.data_ptr()], n) for a, b, o, _ in per]
-        secs = nexr.reduce_copy_multi_device(works, [d for *_, d in per], mg.F32, 0, reps=1)
-        assert secs < 1e-3, secs
+        nexr.reduce_copy_multi_device(works, [d for *_, d in per], mg.F32, 0, reps=1)
+    assert nexr.pool_stats()[0] == created1
+
+
+def test_multi_device_c5_full_size_work_per_gpu(nexr, dev):
+    """one full 256 MiB C2 work (fp32 sum, K=2, M=1) on EVERY visible GPU from one
+    nexrReduceCopyMultiDevice call, each output checked bit-exactly on its own device (fp32 a+b is
+    one IEEE add, so torch's a+b is the oracle's value). On the one-GPU box this is the N=1 case; on a
+    node every GPU runs its own chunk at once."""
+    n = 64 << 20
+    n_dev = torch.cuda.device_count()
+    works, devices, bufs = [], [], []
+    for d in range(n_dev):
+        with torch.cuda.device(d):
+            g = torch.Generator(device=f"cuda:{d}")
+            g.manual_seed(500 + d)
+            a = torch.rand(n, device=f"cuda:{d}", generator=g) * 2 - 1
+            b = torch.rand(n, device=f"cuda:{d}", generator=g) * 2 - 1
+            o = torch.full_like(a, float("nan"))
+            bufs.append((a, b, o))
+            works.append(nexr.make_work([a.data_ptr(), b.data_ptr()], [o.data_ptr()], n))
+            devices.append(d)
+    for d in range(n_dev):
+        torch.cuda.synchronize(d)
+    secs = nexr.reduce_copy_multi_device(works, devices, mg.F32, 0, reps=3)
+    assert secs > 0
+    for d, (a, b, o) in enumerate(bufs):
+        with torch.cuda.device(d):
+            assert torch.equal(o.view(torch.int32), (a + b).view(torch.int32)), f"GPU {d}"

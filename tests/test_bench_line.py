@@ -1,0 +1,130 @@
+"""CPU tests of bench.py's JSON lines (no GPU): the launcher-free N>1 fan-out (one process driving N
+GPUs through nexrReduceCopyMultiDevice) with a faked device count and faked timings, the C5 summary
+arithmetic, and the CPU-baseline core count. The GPU measurement itself runs on the MI355X box."""
+import argparse
+import json
+import types
+
+import pytest
+
+import bench
+
+
+class _FakeWorkload:
+    made = []
+
+    def __init__(self, pkg, cfg, device_index, seed, sets=3):
+        self.device_index = device_index
+        _FakeWorkload.made.append(device_index)
+
+    def work(self, i=0):
+        return ("work", self.device_index)
+
+    def run(self, steps, warmup, dist, per_launch=False):
+        return 0.0, 0.0, 125e-6  # 125 us per launch
+
+    def free(self):
+        pass
+
+
+class _FakePkg:
+    def __init__(self):
+        self.calls = []
+
+    def reduce_copy_multi_device(self, works, devices, dt, op, reps=1):
+        self.calls.append((list(devices), reps))
+        # 0.125 ms per step per GPU alone; 2 % slower with every GPU busy
+        per = 0.125e-3 * (1.02 if len(devices) > 1 else 1.0)
+        return per * reps * (1 + 0.001 * devices[0])
+
+
+def _args(**kw):
+    a = dict(gpus=4, steps=20, warmup=5, config="c2", cpu_seconds=1.0, no_cpu=True, no_h2d=True, no_extra=True,
+             no_xgmi=True, events="region")
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def test_fanout_line_shape(monkeypatch, capsys):
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(bench, "DeviceWorkload", _FakeWorkload)
+    _FakeWorkload.made = []
+    pkg = _FakePkg()
+    cfg = bench.CONFIGS["c2"]
+    res = bench.main_fanout(_args(), cfg, pkg)
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line == json.loads(json.dumps(res))
+    # driver contract keys
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config"):
+        assert key in line, key
+    assert line["n_gpus"] == 4 and line["steps"] == 20 and line["warmup"] == 5 and line["scaling"] == "weak"
+    assert line["metric"] == bench.METRIC and line["dtype"] == "f32"
+    bytes_step = bench.algorithmic_bytes(cfg)
+    agg_s = 0.125e-3 * 1.02 * 20
+    assert line["value"] == pytest.approx(4 * bytes_step * 20 / agg_s / 1e9, rel=1e-4)
+    assert line["ms_per_step"] == pytest.approx(agg_s / 20 * 1e3, abs=1e-4)
+    # all four GPUs together, then each alone, each with W untimed reps first
+    assert pkg.calls[0] == ([0, 1, 2, 3], 5) and pkg.calls[1] == ([0, 1, 2, 3], 20)
+    assert [c for c in pkg.calls[2:]] == [([d], r) for d in range(4) for r in (5, 20)]
+    c5 = line["c5"]
+    assert c5["n1_same_run_gbs"] == pytest.approx(bytes_step * 20 / (0.125e-3 * 20) / 1e9, rel=1e-3)
+    assert len(c5["solo_gbs_per_gpu"]) == 4
+    assert c5["aggregate_over_n_times_n1"] == pytest.approx(1 / 1.02, rel=1e-3)
+    assert line["roofline"]["avg_kernel_us"] == 125.0
+    assert line["roofline"]["frac"] == pytest.approx(bytes_step / 125e-6 / 1e9 / 8000, abs=1e-4)
+    assert "nexrReduceCopyMultiDevice" in line["config"]["parallelism"]
+
+
+def test_fanout_refuses_more_gpus_than_visible(monkeypatch):
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    with pytest.raises(SystemExit):
+        bench.main_fanout(_args(gpus=2), bench.CONFIGS["c2"], _FakePkg())
+
+
+def test_c5_summary_arithmetic():
+    s = bench.c5_summary(8, 1 << 30, 10, agg_seconds=0.02, n1_seconds=0.016, solo_seconds=[0.016] * 8)
+    assert s["aggregate_gbs"] == round(8 * (1 << 30) * 10 / 0.02 / 1e9, 2)
+    assert s["n1_same_run_gbs"] == round((1 << 30) * 10 / 0.016 / 1e9, 2)
+    assert s["aggregate_over_n_times_n1"] == pytest.approx(0.8)
+
+
+def test_usable_cores_is_affinity_capped_by_quota(monkeypatch, tmp_path):
+    import builtins
+    import os
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(128)))
+    real_open = builtins.open
+
+    def fake_open(path, *a, **k):
+        if path == "/sys/fs/cgroup/cpu.max":
+            p = tmp_path / "cpu.max"
+            p.write_text("1600000 100000\n")
+            return real_open(p, *a, **k)
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr(builtins, "open", fake_open)
+    n, how = bench.usable_cores()
+    assert n == 16 and "128" in how and "16" in how
+
+
+def test_cpu_baseline_runs_the_full_configuration(monkeypatch):
+    """The CPU baseline times the benchmarked call itself: every buffer at the config's size."""
+    seen = {}
+    import oracle
+
+    def fake_rc(srcs, m, dt, op, arg, dsts=None, threads=1):
+        seen.setdefault("n", srcs[0].size)
+        seen["threads"] = threads
+        return dsts
+
+    monkeypatch.setattr(oracle, "reduce_copy", fake_rc)
+    cfg = dict(bench.CONFIGS["c4_i8_min"])
+    cfg["buf_bytes"] = 1 << 20  # keep the sample small here; the shape is what is checked
+    e = bench.cpu_baseline_entry(cfg, seconds=0.05)
+    assert seen["n"] == 1 << 20
+    assert e["cores"] == 1 and e["kind"] == "port" and "1 MiB" in e["sample"]
+    assert e["all_cores"]["cores"] == bench.usable_cores()[0] == seen["threads"]
+    assert "1.79" in e["note"]

@@ -1,7 +1,8 @@
 """GPU tests of the process-per-rank peer ring (§8(f) #4): each rank is its own process, FIFOs are
 shared over IPC (hipIpcGetMemHandle / hipIpcOpenMemHandle) and every reduce-copy writes into the
-next rank's FIFO. On the one-GPU test box all ranks share cuda:0, so the peer path is exercised
-through IPC mappings on one device; across GPUs the same mappings go over xGMI.
+next rank's FIFO. Rank r drives GPU r mod (visible GPUs): on a multi-GPU node neighbouring ranks sit
+on different GPUs and every step's write crosses xGMI; on the one-GPU test box all ranks share cuda:0
+and the same IPC mappings stay on the device.
 
 Each rank runs in a child process (tests/peer_ring_worker.py); outputs are compared bit for bit with
 the ring fold-order oracle, for every rank and for a second, in-place call on the same communicator.
@@ -50,6 +51,10 @@ def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="al
         shm_path = "/dev/shm" + name
         if os.path.exists(shm_path):
             os.unlink(shm_path)
+    # Every rank ran on GPU rank mod (visible GPUs): distinct GPUs for neighbours whenever there are two.
+    for r in range(n):
+        ordinal, n_vis = map(int, open(f"{out[r]}.device").read().split())
+        assert ordinal == r % n_vis, (r, ordinal, n_vis)
     return [[np.load(f"{out[r]}.{c}.npy") for c in range(calls)] for r in range(n)]
 
 
@@ -147,3 +152,43 @@ def test_peer_send_recv_processes(tmp_path, n, count):
         for c in range(calls):
             k = (c + 1) % n
             assert outs[r][c].tobytes() == inputs[(r - k) % n].tobytes(), f"rank {r}, call {c}"
+
+
+def test_peer_ring_refuses_a_stale_segment():
+    """Advisor r1: a segment left behind under the same name by a communicator that never left (a
+    crashed run) still holds its ranks' claims and step counters; a new communicator must refuse it
+    (ncclInvalidUsage) instead of inheriting stale head/tail steps."""
+    import ctypes
+    import importlib
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    L = ring.ring_lib()
+    name = f"/nexr_stale_{uuid.uuid4().hex[:12]}".encode()
+    cfg = ring.PeerRingConfig(nRanks=1, rank=0, device=0, buffBytes=1 << 16, protocol=0, timeoutMs=2000,
+                              shmName=name)
+    first, second = ctypes.c_void_p(), ctypes.c_void_p()
+    try:
+        assert L.nexrPeerRingCommCreate(ctypes.byref(first), ctypes.byref(cfg)) == 0
+        # the first communicator is still "alive" in the segment: rank 0's slot is claimed
+        assert L.nexrPeerRingCommCreate(ctypes.byref(second), ctypes.byref(cfg)) == 5
+        # the refused attempt left the live communicator usable
+        x = torch.arange(4096, dtype=torch.float32, device="cuda")
+        y = torch.empty_like(x)
+        assert L.nexrPeerRingAllReduce(first, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), 4096,
+                                       7, 0) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+    finally:
+        if first.value:
+            assert L.nexrRingCommDestroy(first) == 0
+        path = "/dev/shm" + name.decode()
+        if os.path.exists(path):
+            os.unlink(path)
+    # after a clean exit the name is free again
+    try:
+        assert L.nexrPeerRingCommCreate(ctypes.byref(second), ctypes.byref(cfg)) == 0
+    finally:
+        if second.value:
+            L.nexrRingCommDestroy(second)
+        path = "/dev/shm" + name.decode()
+        if os.path.exists(path):
+            os.unlink(path)
