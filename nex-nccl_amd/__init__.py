@@ -126,6 +126,15 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise NexrError(Result.InternalError,
                         f"{LIB_PATH} not built (run __graft_entry__.build() or make -C nex-nccl_amd/csrc)")
+    # One HIP runtime per process. torch ships its own libamdhip64 (soname libamdhip64.so.7, but
+    # NEEDED by torch as "libamdhip64.so"), so loading libnexr first maps /opt/rocm's runtime and
+    # torch then maps a second one: torch's streams and allocations are then foreign handles to
+    # libnexr (hipErrorNoDevice / invalid handle at the first launch). Loading torch first makes
+    # libnexr's NEEDED libamdhip64.so.7 resolve to the runtime torch already mapped.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
     P = ctypes.POINTER

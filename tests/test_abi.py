@@ -8,6 +8,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -284,6 +285,18 @@ def test_package_fails_loudly_without_library(nexr, monkeypatch, tmp_path):
     monkeypatch.setattr(nexr, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(nexr.NexrError):
         nexr.lib()
+
+
+@pytest.mark.parametrize("order", ["lib_first", "torch_first"])
+def test_one_hip_runtime_per_process(order):
+    """libnexr and torch must share ONE libamdhip64: with two, torch's streams are foreign handles to
+    libnexr and the first launch fails (hipError 100 — what bench.py hit when it loaded the library
+    before importing torch). Checked in a fresh interpreter, whichever is loaded first."""
+    body = ("p.lib(); import torch" if order == "lib_first" else "import torch; p.lib()")
+    code = ("import importlib, sys; sys.path.insert(0, %r); p = importlib.import_module('nex-nccl_amd'); %s; "
+            "print(len({l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}))" % (ROOT, body))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True, timeout=300)
+    assert out.stdout.strip().splitlines()[-1] == "1", out.stdout + out.stderr
 
 
 def test_peer_ring_rejects_bad_configs_before_the_device():
