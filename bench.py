@@ -21,6 +21,7 @@ Prints ONE JSON line on rank 0 (keys per the driver contract, plus `roofline`, `
 from __future__ import annotations
 
 import argparse
+import contextlib
 import importlib
 import json
 import os
@@ -76,6 +77,21 @@ def local_device_index() -> int:
     return int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Route fd 1 to fd 2 for the duration (native libraries print there too), so that rank 0's
+    stdout carries exactly the one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class Dist:
     """Barrier, max and gather over the ranks of a torchrun launch. The default backend is gloo: the
     harness needs only host-side synchronisation (each rank synchronises its own GPU first), so the
@@ -94,7 +110,9 @@ class Dist:
             if backend == "nccl":
                 import torch
                 kw["device_id"] = torch.device("cuda", local_device_index())
-            dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world, **kw)
+            with stdout_to_stderr():  # gloo prints its "[Gloo] Rank r is connected to ..." lines on fd 1
+                dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world, **kw)
+                dist.barrier()
             self.pg = dist
 
     def barrier(self):
@@ -458,7 +476,9 @@ def main_ranks(args, cfg, pkg) -> dict | None:
     if dist.rank == 0:
         result = base_line(cfg, dist.world, args.steps, args.warmup, value, max_s,
                            f"independent chunks x{dist.world} (no collective)" +
-                           (f", one process per GPU ({dist.backend} barrier)" if dist.world > 1 else ""))
+                           (f", one process per GPU ({dist.backend} barrier)" if dist.world > 1 else "") +
+                           (f"; REHEARSAL: {dist.world} ranks folded onto {torch.cuda.device_count()} GPU(s)"
+                            if torch.cuda.device_count() < dist.world else ""))
         result["roofline"] = roofline(cfg, args.config, kernel_s, per_launch)
         result["cpu_baseline"] = None
         result["h2d_inclusive"] = None
@@ -488,13 +508,16 @@ def main_fanout(args, cfg, pkg) -> dict:
     import torch
 
     n_vis = torch.cuda.device_count()
-    if n_vis < args.gpus:
+    # NEXR_BENCH_FOLD=1 folds the N chunks onto the visible GPUs (chunk d on GPU d mod n): a rehearsal
+    # of this path on a box with fewer GPUs; the line then says so in config.parallelism.
+    fold = os.environ.get("NEXR_BENCH_FOLD") == "1"
+    if n_vis < args.gpus and not fold:
         raise SystemExit(f"--gpus {args.gpus} but only {n_vis} visible GPU(s)")
-    wls = [DeviceWorkload(pkg, cfg, d, seed=1000 + d, sets=1) for d in range(args.gpus)]
-    for d in range(args.gpus):
+    devices = [d % n_vis for d in range(args.gpus)]
+    wls = [DeviceWorkload(pkg, cfg, dev, seed=1000 + d, sets=1) for d, dev in enumerate(devices)]
+    for d in sorted(set(devices)):
         torch.cuda.synchronize(d)
     works = [wl.work(0) for wl in wls]
-    devices = list(range(args.gpus))
     bytes_step = algorithmic_bytes(cfg)
 
     def timed(ws, ds):
@@ -502,11 +525,12 @@ def main_fanout(args, cfg, pkg) -> dict:
         return pkg.reduce_copy_multi_device(ws, ds, cfg["dt"], cfg["op"], reps=args.steps)
 
     agg_s = timed(works, devices)
-    solo = [timed([works[d]], [d]) for d in devices]
+    solo = [timed([works[i]], [devices[i]]) for i in range(args.gpus)]
     value = args.gpus * bytes_step * args.steps / agg_s / 1e9
     result = base_line(cfg, args.gpus, args.steps, args.warmup, value, agg_s,
                        f"independent chunks x{args.gpus} (no collective), one process, "
-                       f"nexrReduceCopyMultiDevice (a host thread + stream per GPU)")
+                       f"nexrReduceCopyMultiDevice (a host thread + stream per GPU)" +
+                       (f"; REHEARSAL: {args.gpus} chunks folded onto {n_vis} GPU(s)" if n_vis < args.gpus else ""))
     # Roofline of the kernel itself: HIP events on GPU 0's launch stream, 3 rotating sets.
     for wl in wls:
         wl.free()

@@ -118,6 +118,17 @@ class ReduceCopyWork(ctypes.Structure):
 _lib = None
 
 
+def hip_runtime() -> ctypes.CDLL:
+    """The HIP runtime libnexr runs on (the one libamdhip64 mapped in this process, see lib()), for
+    harness calls the ABI does not cover (hipDeviceEnablePeerAccess in tools/xgmi_probe.py)."""
+    lib()
+    with open("/proc/self/maps") as f:
+        paths = sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln and "/" in ln})
+    if len(paths) != 1:
+        raise NexrError(Result.InternalError, f"expected one HIP runtime in the process, found {paths}")
+    return ctypes.CDLL(paths[0])
+
+
 def lib() -> ctypes.CDLL:
     """Load libnexr.so (raises if it is missing: there is no CPU fallback)."""
     global _lib

@@ -332,3 +332,12 @@ def test_multi_device_c_example_builds(monkeypatch):
     import __graft_entry__
     exe = __graft_entry__.build_c_multi_device()
     assert os.path.exists(exe) and os.access(exe, os.X_OK)
+
+
+def test_hip_runtime_is_the_one_libnexr_uses(nexr):
+    """nexr.hip_runtime() hands back the single mapped libamdhip64 (harness calls such as
+    hipDeviceEnablePeerAccess must reach the runtime the kernels launch on)."""
+    h = nexr.hip_runtime()
+    mapped = {ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln and "/" in ln}
+    assert mapped == {h._name}
+    assert hasattr(h, "hipDeviceEnablePeerAccess")

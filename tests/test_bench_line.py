@@ -85,6 +85,22 @@ def test_fanout_refuses_more_gpus_than_visible(monkeypatch):
         bench.main_fanout(_args(gpus=2), bench.CONFIGS["c2"], _FakePkg())
 
 
+def test_fanout_rehearsal_folds_chunks_onto_visible_gpus(monkeypatch, capsys):
+    """NEXR_BENCH_FOLD=1: 2 chunks on a 1-GPU box both run on GPU 0 and the line says REHEARSAL."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(bench, "DeviceWorkload", _FakeWorkload)
+    monkeypatch.setenv("NEXR_BENCH_FOLD", "1")
+    _FakeWorkload.made = []
+    pkg = _FakePkg()
+    bench.main_fanout(_args(gpus=2), bench.CONFIGS["c2"], pkg)
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert pkg.calls[0] == ([0, 0], 5) and pkg.calls[2:] == [([0], 5), ([0], 20)] * 2
+    assert "REHEARSAL: 2 chunks folded onto 1 GPU(s)" in line["config"]["parallelism"]
+    assert line["n_gpus"] == 2
+
+
 def test_c5_summary_arithmetic():
     s = bench.c5_summary(8, 1 << 30, 10, agg_seconds=0.02, n1_seconds=0.016, solo_seconds=[0.016] * 8)
     assert s["aggregate_gbs"] == round(8 * (1 << 30) * 10 / 0.02 / 1e9, 2)

@@ -63,3 +63,24 @@ def test_two_rank_independent_chunks_max_timer():
     assert g0 == g1 == [[l0, 0.0], [l1, 1.0]]
     assert s0 == s1 and len(s0["wall_gbs"]) == 2
     assert s0["min_wall_gbs"] == round(5 * (1 << 20) / l1 / 1e9, 2)  # the slow rank sets the minimum
+
+
+def test_rank_stdout_is_only_the_json_line(tmp_path):
+    """gloo's native "[Gloo] Rank r is connected to ..." lines go to fd 1; bench.Dist routes them to
+    stderr so that rank 0's stdout under torchrun is exactly the driver's one JSON line."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "rank.py"
+    script.write_text(f"import sys; sys.path.insert(0, {root!r}); import bench\n"
+                      "d = bench.Dist('gloo'); print('{\"rank\": %d}' % d.rank); d.close()\n")
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert [o for o, _ in outs] == ['{"rank": 0}\n', '{"rank": 1}\n']

@@ -35,7 +35,8 @@ def main() -> int:
     if not torch.cuda.can_device_access_peer(0, 1):
         print(json.dumps({"skipped": "GPU 0 cannot access GPU 1's memory"}), flush=True)
         return 0
-    hip = ctypes.CDLL("libamdhip64.so")
+    pkg = importlib.import_module("nex-nccl_amd")
+    hip = pkg.hip_runtime()  # the runtime torch and libnexr share, not a second copy
     for a, b in ((0, 1), (1, 0)):
         torch.cuda.set_device(a)
         rc = hip.hipDeviceEnablePeerAccess(ctypes.c_int(b), ctypes.c_uint(0))
@@ -43,8 +44,6 @@ def main() -> int:
             print(json.dumps({"skipped": f"hipDeviceEnablePeerAccess({a}->{b}) = {rc}"}), flush=True)
             return 0
     hip.hipGetLastError()
-    pkg = importlib.import_module("nex-nccl_amd")
-    pkg.lib()
     n = 64 << 20  # fp32 elements: 256 MiB per buffer
     torch.cuda.set_device(0)
     d0, d1 = torch.device("cuda", 0), torch.device("cuda", 1)
