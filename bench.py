@@ -274,6 +274,52 @@ def extra_configs(pkg, steps: int = 20, warmup: int = 5, names=EXTRA_ORDER) -> d
     return out
 
 
+# ---- C1: the emulated ring all-reduce (BASELINE configs[0]) -------------------------------------
+def c1_ring(iters: int = 20) -> dict:
+    """BASELINE configs[0]: fp32 sum all-reduce of 4 MiB per rank over 2 emulated ranks, the ring
+    schedule (runRing, src/device/all_reduce.h:12-84) with SIMPLE steps, restated in libnexr_ring.
+    Three reduce-copy back ends under the same schedule: the HIP kernel on device-resident buffers,
+    the HIP kernel behind host staging buffers (the fork's setting: NEX "device memory" is host
+    memory), and the CPU oracle (every step on a host core, the reference's own path). Inputs are
+    small integers, so every fold order gives the same fp32 sums and each result is checked exactly."""
+    import ctypes
+    import numpy as np
+    import torch
+    import oracle
+
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    n, count = 2, 1 << 20
+    rng = np.random.default_rng(1)
+    x = [rng.integers(-1000, 1000, count).astype(np.float32) for _ in range(n)]
+    expect = x[0] + x[1]
+    ol = oracle.lib()
+    cpu_fn = ctypes.cast(ol.oracle_reduce_copy_fn, ctypes.c_void_p).value
+    out = {"workload": "fp32 sum all-reduce, 4 MiB per rank, 2 emulated ranks, ring SIMPLE, 1 channel"}
+    for name, mode, fn in (("device", ring.DEVICE_MEMORY, None), ("host_staged", ring.HOST_MEMORY, None),
+                           ("cpu_oracle", ring.HOST_MEMORY, cpu_fn)):
+        if mode == ring.DEVICE_MEMORY:
+            send = [torch.from_numpy(v).cuda() for v in x]
+            recv = [torch.zeros(count, dtype=torch.float32, device="cuda") for _ in range(n)]
+            torch.cuda.synchronize()
+        else:
+            send, recv = [v.copy() for v in x], [np.zeros(count, np.float32) for _ in range(n)]
+        sp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in send]
+        rp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in recv]
+        reps = iters if fn is None else max(2, iters // 10)
+        with ring.RingComm(n, mode, 0, fn) as comm:
+            comm.all_reduce(sp, rp, count, 7, 0)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                comm.all_reduce(sp, rp, count, 7, 0)
+            dt = (time.perf_counter() - t0) / reps
+        got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
+        out[name] = {"ms_per_call": round(dt * 1e3, 3), "algbw_gbs": round(count * 4 / dt / 1e9, 2), "calls": reps,
+                     "exact": all(np.array_equal(g, expect) for g in got)}
+    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); cpu_oracle runs the same schedule with the "
+                   "C restatement as its reduce-copy on host cores")
+    return out
+
+
 # ---- CPU baseline: the oracle (C restatement) on the benchmarked configuration ------------------
 def usable_cores() -> tuple:
     """(threads to use, how that was decided): the CPUs this process may run on, capped by the
@@ -486,6 +532,7 @@ def main_ranks(args, cfg, pkg) -> dict | None:
             if not args.no_extra:
                 wl.free()
                 result["extra_configs"] = extra_configs(pkg)
+                result["c1_ring"] = c1_ring()
             if not args.no_cpu:
                 result["cpu_baseline"] = cpu_baseline_entry(cfg, args.cpu_seconds)
             if not args.no_h2d:

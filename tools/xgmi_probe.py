@@ -89,34 +89,41 @@ def main() -> int:
     return 0
 
 
+PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2}
+LL_COUNT = 1 << 20  # the LL protocols run C1's 4 MiB only (they move 2x / 16/15x the payload)
+
+
 def ring_rank(rank: int, shm: str, counts) -> int:
-    """One rank of the cross-GPU process ring (child process, GPU `rank`)."""
+    """One rank of the cross-GPU process ring (child process, GPU `rank`): the SIMPLE ring at every
+    count, then the LL and LL128 rings at C1's size, one communicator per protocol."""
     import time
     import torch
     dev = rank % torch.cuda.device_count()  # GPU r; both on GPU 0 when rehearsing on a one-GPU box
     torch.cuda.set_device(dev)
     ring = importlib.import_module("nex-nccl_amd.ring")
-    res = {}
-    with ring.PeerRingComm(2, rank, shm, device=dev, timeout_ms=30000) as comm:
-        for count in counts:
-            x = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) + rank
-            y = torch.empty_like(x)
-            exp = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) * 2 + 1
-            torch.cuda.synchronize()
-            comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)  # warm-up, connects the FIFOs
-            iters = 5
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)
-            dt = (time.perf_counter() - t0) / iters
-            res[str(count * 4)] = {"ms": round(dt * 1e3, 3), "algbw_GBps": round(count * 4 / dt / 1e9, 2),
-                                   "exact": bool(torch.equal(y, exp))}
+    out = {}
+    for pname, proto in PROTOCOLS.items():
+        out[pname] = res = {}
+        with ring.PeerRingComm(2, rank, f"{shm}_{pname}", device=dev, protocol=proto, timeout_ms=30000) as comm:
+            for count in (counts if pname == "simple" else [LL_COUNT]):
+                x = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) + rank
+                y = torch.empty_like(x)
+                exp = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) * 2 + 1
+                torch.cuda.synchronize()
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)  # warm-up, connects the FIFOs
+                iters = 5
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)
+                dt = (time.perf_counter() - t0) / iters
+                res[str(count * 4)] = {"ms": round(dt * 1e3, 3), "algbw_GBps": round(count * 4 / dt / 1e9, 2),
+                                       "exact": bool(torch.equal(y, exp))}
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(out), flush=True)
     return 0
 
 
-def ring_processes(timeout_s: float = 45.0):
+def ring_processes(timeout_s: float = 60.0):
     import subprocess
     import uuid
     shm = f"/nexr_xgmi_{uuid.uuid4().hex[:12]}"
@@ -135,12 +142,14 @@ def ring_processes(timeout_s: float = 45.0):
                 p.wait()
         return {"error": "timeout"}
     finally:
-        if os.path.exists("/dev/shm" + shm):
-            os.unlink("/dev/shm" + shm)
+        for pname in PROTOCOLS:
+            if os.path.exists(f"/dev/shm{shm}_{pname}"):
+                os.unlink(f"/dev/shm{shm}_{pname}")
     if any(p.returncode != 0 for p in procs):
         return {"error": [p.returncode for p in procs], "stderr": [e[-300:] for _, e in outs]}
     lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
-    return {"per_rank_bytes": json.loads(lines[-1]), "ranks": "2 processes, rank r on GPU r, SIMPLE, fp32 sum"}
+    return {"per_protocol_bytes": json.loads(lines[-1]),
+            "ranks": "2 processes, rank r on GPU r, fp32 sum; SIMPLE at 4 and 64 MiB, LL and LL128 at 4 MiB"}
 
 
 if __name__ == "__main__":
