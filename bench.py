@@ -297,10 +297,13 @@ def c1_ring(iters: int = 20) -> dict:
     out = {"workload": "fp32 sum all-reduce, 4 MiB per rank, 2 emulated ranks, ring SIMPLE, 1 channel"}
     for name, mode, fn in (("device", ring.DEVICE_MEMORY, None), ("host_staged", ring.HOST_MEMORY, None),
                            ("cpu_oracle", ring.HOST_MEMORY, cpu_fn)):
-        if mode == ring.DEVICE_MEMORY:
-            send = [torch.from_numpy(v).cuda() for v in x]
-            recv = [torch.zeros(count, dtype=torch.float32, device="cuda") for _ in range(n)]
-            torch.cuda.synchronize()
+        if mode == ring.DEVICE_MEMORY:  # rank r's buffers on rank r's GPU (libnexr_ring: r mod visible)
+            devs = [torch.device("cuda", r % torch.cuda.device_count()) for r in range(n)]
+            send = [torch.from_numpy(v).to(d) for v, d in zip(x, devs)]
+            recv = [torch.zeros(count, dtype=torch.float32, device=d) for d in devs]
+            for d in set(devs):
+                torch.cuda.synchronize(d)
+            out["device_gpus"] = [d.index for d in devs]
         else:
             send, recv = [v.copy() for v in x], [np.zeros(count, np.float32) for _ in range(n)]
         sp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in send]
