@@ -270,8 +270,9 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
                                       size_t nElts, int datatype, nexrLaunchInfo* info);
 
 /* Diagnostics: how many streams nexrReduceCopyMultiDevice and how many staging rings
- * nexrReduceCopyHost have created in this process so far (both are pooled and reused, so the counts
- * stop growing once the pools are warm). Either pointer may be NULL. */
+ * nexrReduceCopyHost have created in this process so far (device rings of the chunk pipeline plus
+ * pinned rings of the large-call copy-team path; all pooled and reused, so the counts stop growing
+ * once the pools are warm). Either pointer may be NULL. */
 NEXR_API nexrResult_t nexrGetPoolStats(uint64_t* multiDeviceStreams, uint64_t* hostStagingRings);
 
 /* Bytes per element of a datatype (reference ncclTypeSize), 0 if unknown. */

@@ -5,6 +5,7 @@
 #include <string.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -461,6 +462,242 @@ nexrResult_t stageFor(size_t slotBytes, hipStream_t caller, StageLease* lease) {
   return nexrSuccess;
 }
 
+// ---- host-staged variant, large pageable calls: a CPU copy team and pinned zero-copy slots -------
+// The runtime's pageable hipMemcpyAsync copies through its own staging buffer with one CPU memcpy
+// before each DMA, which held the C2 mix to 49 GB/s against an ~86 GB/s PCIe floor
+// (profiles/r01_h2d_probe.log). For a call with at least NEXR_HOST_MT_MIN_BYTES of pageable
+// buffers: a team of host threads copies each chunk of the pageable sources into a pinned,
+// device-mapped slot; the kernel reads the slot and writes its output slot in place over PCIe
+// (zero-copy, both link directions at once; pinned user buffers are read/written in place as
+// well); the team copies the output slot to the pageable destinations. Three slots: chunk c is
+// filled while chunk c-1 is reduced and chunk c-2 is drained.
+constexpr int kPinnedSlots = 3;
+struct PinnedStage {
+  int device = -1;
+  char* host = nullptr;  // hipHostMalloc (pinned, mapped, coherent): kPinnedSlots x slotBytes
+  char* dev = nullptr;   // the same bytes as the device addresses them
+  size_t slotBytes = 0;
+  hipEvent_t done[kPinnedSlots] = {};
+};
+std::mutex gPinMu;
+std::vector<PinnedStage*> gPinIdle;
+uint64_t gPinCreated = 0;  // under gPinMu (nexrGetPoolStats)
+
+// Checks a pinned ring out for the current device; the lease drains every slot's last kernel before
+// handing the ring back (a ring whose events report an error is dropped, not reused).
+struct PinLease {
+  PinnedStage* st = nullptr;
+  ~PinLease() {
+    if (!st) return;
+    bool ok = true;
+    for (int i = 0; i < kPinnedSlots; i++) ok = hipEventSynchronize(st->done[i]) == hipSuccess && ok;
+    if (!ok) {
+      (void)hipGetLastError();
+      return;
+    }
+    std::lock_guard<std::mutex> g(gPinMu);
+    gPinIdle.push_back(st);
+  }
+};
+
+nexrResult_t pinnedFor(size_t slotBytes, PinLease* lease) {
+  int dev = 0;
+  NEXR_HIP(hipGetDevice(&dev));
+  PinnedStage* st = nullptr;
+  {
+    std::lock_guard<std::mutex> g(gPinMu);
+    for (size_t i = 0; i < gPinIdle.size(); i++)
+      if (gPinIdle[i]->device == dev && (!st || gPinIdle[i]->slotBytes > st->slotBytes)) st = gPinIdle[i];
+    if (st) gPinIdle.erase(std::find(gPinIdle.begin(), gPinIdle.end(), st));
+  }
+  if (!st) {
+    st = new PinnedStage();
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < kPinnedSlots && e == hipSuccess; i++)
+      e = hipEventCreateWithFlags(&st->done[i], hipEventDisableTiming);
+    if (e == hipSuccess) {  // the events start "complete": record each once on the null stream
+      for (int i = 0; i < kPinnedSlots && e == hipSuccess; i++) e = hipEventRecord(st->done[i], nullptr);
+    }
+    if (e != hipSuccess) {
+      for (int i = 0; i < kPinnedSlots; i++)
+        if (st->done[i]) (void)hipEventDestroy(st->done[i]);
+      delete st;
+      return hipFail(e);
+    }
+    st->device = dev;
+    std::lock_guard<std::mutex> g(gPinMu);
+    gPinCreated++;
+  }
+  lease->st = st;
+  if (st->slotBytes < slotBytes) {  // idle ring: its events were synchronised when it was handed back
+    if (st->host) NEXR_HIP(hipHostFree(st->host));
+    st->host = st->dev = nullptr;
+    st->slotBytes = 0;
+    NEXR_HIP(hipHostMalloc((void**)&st->host, kPinnedSlots * slotBytes, hipHostMallocDefault));
+    NEXR_HIP(hipHostGetDevicePointer((void**)&st->dev, st->host, 0));
+    st->slotBytes = slotBytes;
+  }
+  return nexrSuccess;
+}
+
+// Parallel memcpy: `run` splits every task into one contiguous, 4 KiB-aligned piece per thread and
+// returns when all pieces are copied. The calling thread copies a piece too; the others are
+// created for one host call and joined when it ends.
+class CopyTeam {
+ public:
+  struct Task {
+    char* dst;
+    const char* src;
+    size_t bytes;
+  };
+  explicit CopyTeam(int n) {
+    for (int i = 1; i < n; i++) {
+      try {
+        workers_.emplace_back([this, i] { loop(i); });
+      } catch (...) {  // fewer threads than asked for: the pieces are re-split over those that exist
+        break;
+      }
+    }
+    n_ = 1 + (int)workers_.size();
+  }
+  ~CopyTeam() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  void run(const Task* tasks, int nTasks) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      tasks_ = tasks;
+      nTasks_ = nTasks;
+      pending_ = n_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    piece(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void piece(int idx) const {
+    for (int t = 0; t < nTasks_; t++) {
+      const Task& k = tasks_[t];
+      const size_t per = ((k.bytes + n_ - 1) / n_ + 4095) & ~(size_t)4095;
+      const size_t b0 = per * (size_t)idx;
+      if (b0 >= k.bytes) continue;
+      memcpy(k.dst + b0, k.src + b0, per < k.bytes - b0 ? per : k.bytes - b0);
+    }
+  }
+  void loop(int idx) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      piece(idx);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> workers_;
+  int n_ = 1;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+  const Task* tasks_ = nullptr;
+  int nTasks_ = 0;
+};
+
+// srcs/dsts: the caller's host pointers; psrc/pdst: which are pinned (zsrc/zdst: their device
+// addresses, used in place).
+nexrResult_t reduceCopyHostTeam(int nSrcs, const void* const* srcs, const bool* psrc, const void* const* zsrc,
+                                int nDsts, void* const* dsts, const bool* pdst, void* const* zdst, size_t nElts,
+                                int datatype, int op, uint64_t redOpArg, int nPreOpSrcs, const uint64_t* preOpArgs,
+                                int postOp, hipStream_t s, int nThreads) {
+  const size_t esz = typeSize(datatype);
+  static const long chunkOverride = envLong("NEXR_HOST_MT_CHUNK_BYTES", 32l << 20);
+  size_t chunkElts = ((size_t)(chunkOverride > 4096 ? chunkOverride : 4096) / esz) & ~(size_t)15;
+  if (chunkElts > nElts) chunkElts = nElts;
+  const size_t chunkBytes = ((chunkElts * esz) + 4095) & ~(size_t)4095;
+  int nPageSrc = 0;
+  bool outStaged = false;
+  for (int k = 0; k < nSrcs; k++) nPageSrc += psrc[k] ? 0 : 1;
+  for (int d = 0; d < nDsts; d++) outStaged |= !pdst[d];
+  PinLease lease;
+  nexrResult_t r = pinnedFor(chunkBytes * (size_t)(nPageSrc + (outStaged ? 1 : 0)), &lease);
+  if (r != nexrSuccess) return r;
+  PinnedStage* st = lease.st;
+  CopyTeam team(nThreads);
+  const size_t nChunks = (nElts + chunkElts - 1) / chunkElts;
+  auto span = [&](size_t c, size_t* e0, size_t* n) {
+    *e0 = c * chunkElts;
+    *n = nElts - *e0 < chunkElts ? nElts - *e0 : chunkElts;
+  };
+  auto outOffset = [&] { return chunkBytes * (size_t)nPageSrc; };
+  // Copy-in tasks of chunk c (its pageable sources into slot c % 3) and copy-out tasks of chunk c
+  // (slot c % 3's output to the pageable destinations), appended to `tasks`.
+  CopyTeam::Task tasks[NEXR_MAX_SRCS + NEXR_MAX_DSTS];
+  int nTasks = 0;
+  auto copyIn = [&](size_t c) {
+    size_t e0, n;
+    span(c, &e0, &n);
+    const size_t slot = (c % kPinnedSlots) * st->slotBytes;
+    for (int k = 0, j = 0; k < nSrcs; k++)
+      if (!psrc[k]) tasks[nTasks++] = {st->host + slot + chunkBytes * j++, (const char*)srcs[k] + e0 * esz, n * esz};
+  };
+  auto copyOut = [&](size_t c) {
+    size_t e0, n;
+    span(c, &e0, &n);
+    const char* out = st->host + (c % kPinnedSlots) * st->slotBytes + outOffset();
+    for (int d = 0; d < nDsts; d++)
+      if (!pdst[d]) tasks[nTasks++] = {(char*)dsts[d] + e0 * esz, out, n * esz};
+  };
+  auto launch = [&](size_t c) -> nexrResult_t {
+    size_t e0, n;
+    span(c, &e0, &n);
+    const size_t slot = (c % kPinnedSlots) * st->slotBytes;
+    const void* dsrc[NEXR_MAX_SRCS];
+    for (int k = 0, j = 0; k < nSrcs; k++)
+      dsrc[k] = psrc[k] ? (const void*)((const char*)zsrc[k] + e0 * esz) : (const void*)(st->dev + slot + chunkBytes * j++);
+    void* ddst[NEXR_MAX_DSTS + 1];
+    int m = 0;
+    for (int d = 0; d < nDsts; d++)
+      if (pdst[d]) ddst[m++] = (char*)zdst[d] + e0 * esz;
+    if (outStaged) ddst[m++] = st->dev + slot + outOffset();
+    nexrResult_t rr = reduceCopyDevice(nSrcs, dsrc, m, ddst, n, datatype, op, redOpArg, nPreOpSrcs, preOpArgs,
+                                       nullptr, postOp, s);
+    if (rr != nexrSuccess) return rr;
+    NEXR_HIP(hipEventRecord(st->done[c % kPinnedSlots], s));
+    return nexrSuccess;
+  };
+  // Iteration c: wait for chunk c-2's kernel, then ONE team pass copies chunk c-2's output out of
+  // slot (c-2) % 3 and chunk c's sources into slot c % 3 (drained one iteration ago) while the GPU
+  // reduces chunk c-1; then chunk c's kernel is queued.
+  for (size_t c = 0; c < nChunks + 2; c++) {
+    nTasks = 0;
+    if (c >= 2) {
+      NEXR_HIP(hipEventSynchronize(st->done[(c - 2) % kPinnedSlots]));
+      if (outStaged) copyOut(c - 2);
+    }
+    if (c < nChunks) copyIn(c);
+    if (nTasks > 0) team.run(tasks, nTasks);
+    if (c < nChunks) {
+      r = launch(c);
+      if (r != nexrSuccess) return r;
+    }
+  }
+  return nexrSuccess;
+}
+
 // ---- host-side half/bfloat16 rounding used by the op encoder (RNE, NaN -> 0x7fff) ------------
 uint16_t floatToHalfRne(float f) {
   uint32_t x;
@@ -513,8 +750,13 @@ NEXR_API nexrResult_t nexrGetPoolStats(uint64_t* multiDeviceStreams, uint64_t* h
     *multiDeviceStreams = gMdStreamsCreated;
   }
   if (hostStagingRings) {
-    std::lock_guard<std::mutex> g(gStageMu);
-    *hostStagingRings = gStagesCreated;
+    uint64_t n = 0;
+    {
+      std::lock_guard<std::mutex> g(gStageMu);
+      n = gStagesCreated;
+    }
+    std::lock_guard<std::mutex> g(gPinMu);
+    *hostStagingRings = n + gPinCreated;
   }
   return nexrSuccess;
 }
@@ -591,9 +833,15 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
     NEXR_HIP(hipStreamSynchronize(s));
     return nexrSuccess;
   }
+  const size_t esz = typeSize(datatype);
+  // Large calls: the CPU copy team into pinned zero-copy slots (reduceCopyHostTeam).
+  static const long mtMin = envLong("NEXR_HOST_MT_MIN_BYTES", 32l << 20);
+  static const long mtThreads = envLong("NEXR_HOST_COPY_THREADS", 8);
+  if (mtThreads > 1 && (uint64_t)(nSrcs + nDsts - nPinned) * nElts * esz >= (uint64_t)mtMin)
+    return reduceCopyHostTeam(nSrcs, srcs, psrc, zsrc, nDsts, dsts, pdst, zdst, nElts, datatype, devRedOp, redOpArg,
+                              nPreOpSrcs, preOpArgs, postOp, s, (int)(mtThreads > 64 ? 64 : mtThreads));
   // Some buffers pageable: a two-stream chunk pipeline through device memory for those only; the
   // pinned ones (e.g. the emulated transport's FIFOs) are read and written in place by the kernel.
-  const size_t esz = typeSize(datatype);
   static const long chunkOverride = envLong("NEXR_HOST_CHUNK_BYTES", 8l << 20);
   size_t chunkElts = ((size_t)(chunkOverride > 4096 ? chunkOverride : 4096) / esz) & ~(size_t)15;
   if (chunkElts > nElts) chunkElts = nElts;

@@ -315,6 +315,27 @@ def test_buffers_larger_than_4gib(nexr, dev):
     torch.cuda.empty_cache()
 
 
+def test_generic_path_beyond_the_work_item_limit(nexr, dev):
+    """Advisor r1, on hardware: pointers with different 16-B phases take the per-element (generic)
+    path, one element per work item, so a call with more than 2^32 - 1 elements needs more work items
+    than HIP launches. The grid is capped at (2^32 - 1) / block (nexrQueryLaunch shows it) and the
+    kernel grid-strides over the rest: 2^32 + 4099 uint8 elements, src1 one byte off src0's phase."""
+    n = (1 << 32) + 4099
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    a = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    braw = torch.randint(0, 256, (n + 1,), dtype=torch.uint8, device="cuda", generator=g)
+    b = braw[1:]  # 16-B phase 1 against a's phase 0: no common alignment
+    o = torch.empty_like(a)
+    info = nexr.query_launch([a.data_ptr(), b.data_ptr()], [o.data_ptr()], n, nexr.DataType.Uint8)
+    assert info.generic == 1 and info.grid * info.block <= 0xFFFFFFFF < n
+    nexr.reduce_copy([a, b], [o], nexr.DevRedOp.Sum, datatype=nexr.DataType.Uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(o, a + b)
+    del a, braw, b, o
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("dt,n,op,name", [(mg.F32, 5_000_003, mg.SUM, "sum"), (mg.I8, 30_000_001, mg.MINMAX, "max"),
                                           (mg.BF16, 9_000_017, mg.PROD, "prod")])
 def test_host_staged_pipeline_multi_chunk(nexr, oracle, dt, n, op, name, dev):
