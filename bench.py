@@ -463,7 +463,8 @@ def h2d_inclusive(pkg, cfg, reps: int = 3):
     """Rate with the host<->device traffic included (nexrReduceCopyHost on host buffers).
 
     Pinned buffers take the zero-copy path (the kernel reads/writes host memory over PCIe, both
-    directions at once); pageable buffers take the staged two-stream chunk pipeline."""
+    directions at once); pageable buffers of a call this large go through the host copy team into
+    pinned zero-copy slots (nexr_api.cpp reduceCopyHostTeam)."""
     import numpy as np
     import torch
 
@@ -492,7 +493,9 @@ def h2d_inclusive(pkg, cfg, reps: int = 3):
     return {"value": round(alg / t_pin / 1e9, 2), "unit": "GB/s", "ms_per_call": round(t_pin * 1e3, 3),
             "path": "nexrReduceCopyHost, pinned host buffers: zero-copy kernel over PCIe Gen5 x16",
             "pageable": {"value": round(alg / t_page / 1e9, 2), "ms_per_call": round(t_page * 1e3, 3),
-                         "path": "staged H2D -> kernel -> D2H, two-stream 8 MiB chunk pipeline"}}
+                         "path": "host copy team (8 threads) into pinned zero-copy slots, 32 MiB chunks, "
+                                 "kernel over PCIe, copy team out (calls under 32 MiB: the runtime's "
+                                 "H2D -> kernel -> D2H two-stream chunk pipeline)"}}
 
 
 # ---- the two ways to drive N GPUs ---------------------------------------------------------------
