@@ -1,6 +1,6 @@
 // How the HBM read rate depends on the number of concurrent input streams read at the same
 // offsets (the access shape of a K-input reduce-copy), with and without the output stream.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/streams.hip -o tools/streams
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DNEXR_DT=7 tools/streams.hip -o tools/streams
 #include "../nex-nccl_amd/csrc/nexr_kernels.hip"
 #include <algorithm>
 #include <cstdio>
