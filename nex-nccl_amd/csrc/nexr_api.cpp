@@ -483,13 +483,15 @@ std::mutex gPinMu;
 std::vector<PinnedStage*> gPinIdle;
 uint64_t gPinCreated = 0;  // under gPinMu (nexrGetPoolStats)
 
-// Checks a pinned ring out for the current device; the lease drains every slot's last kernel before
-// handing the ring back (a ring whose events report an error is dropped, not reused).
+// Checks a pinned ring out for the current device; the lease drains the caller's stream (every
+// kernel this call queued, even one whose completion event could not be recorded) and every slot's
+// event before handing the ring back; a ring that reports an error is dropped, not reused.
 struct PinLease {
   PinnedStage* st = nullptr;
+  hipStream_t caller = nullptr;
   ~PinLease() {
     if (!st) return;
-    bool ok = true;
+    bool ok = hipStreamSynchronize(caller) == hipSuccess;
     for (int i = 0; i < kPinnedSlots; i++) ok = hipEventSynchronize(st->done[i]) == hipSuccess && ok;
     if (!ok) {
       (void)hipGetLastError();
@@ -500,7 +502,7 @@ struct PinLease {
   }
 };
 
-nexrResult_t pinnedFor(size_t slotBytes, PinLease* lease) {
+nexrResult_t pinnedFor(size_t slotBytes, hipStream_t caller, PinLease* lease) {
   int dev = 0;
   NEXR_HIP(hipGetDevice(&dev));
   PinnedStage* st = nullptr;
@@ -529,6 +531,7 @@ nexrResult_t pinnedFor(size_t slotBytes, PinLease* lease) {
     gPinCreated++;
   }
   lease->st = st;
+  lease->caller = caller;
   if (st->slotBytes < slotBytes) {  // idle ring: its events were synchronised when it was handed back
     if (st->host) NEXR_HIP(hipHostFree(st->host));
     st->host = st->dev = nullptr;
@@ -633,7 +636,7 @@ nexrResult_t reduceCopyHostTeam(int nSrcs, const void* const* srcs, const bool* 
   for (int k = 0; k < nSrcs; k++) nPageSrc += psrc[k] ? 0 : 1;
   for (int d = 0; d < nDsts; d++) outStaged |= !pdst[d];
   PinLease lease;
-  nexrResult_t r = pinnedFor(chunkBytes * (size_t)(nPageSrc + (outStaged ? 1 : 0)), &lease);
+  nexrResult_t r = pinnedFor(chunkBytes * (size_t)(nPageSrc + (outStaged ? 1 : 0)), s, &lease);
   if (r != nexrSuccess) return r;
   PinnedStage* st = lease.st;
   CopyTeam team(nThreads);
