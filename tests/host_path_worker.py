@@ -16,8 +16,45 @@ import make_golden as mg  # noqa: E402
 import oracle  # noqa: E402
 
 
+def concurrent(nexr) -> int:
+    """Eight host threads at once, each with its own pageable buffers: every call checks a staging
+    ring out of the pool and returns it, so the pool ends with at most one ring per concurrent call."""
+    import threading
+    n = 2_000_003
+    srcs = mg.gen_inputs(mg.F32, 3, n, 777, special=True)
+    exp = oracle.reduce_copy(srcs, 1, mg.F32, mg.SUM, threads=8)[0]
+    errors = []
+
+    def call(t):
+        try:
+            torch.cuda.set_device(0)
+            mine = [s.copy() for s in srcs]
+            for _ in range(3):
+                d = np.zeros_like(srcs[0])
+                nexr.reduce_copy_ptrs([m.ctypes.data for m in mine], [d.ctypes.data], n, mg.F32, mg.SUM, host=True)
+                if mg.canon_bytes(mg.F32, d) != mg.canon_bytes(mg.F32, exp):
+                    errors.append(f"thread {t}: mismatch")
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=call, args=(t,)) for t in range(8)]
+    [t.start() for t in ths]
+    [t.join(timeout=120) for t in ths]
+    if any(t.is_alive() for t in ths) or errors:
+        print("CONCURRENT FAILURE", errors[:3], flush=True)
+        return 1
+    streams, rings = nexr.pool_stats()
+    if rings > 8:
+        print(f"POOL: {rings} rings for 8 concurrent callers", flush=True)
+        return 1
+    print("host-path ok concurrent", (streams, rings), flush=True)
+    return 0
+
+
 def main() -> int:
     nexr = importlib.import_module("nex-nccl_amd")
+    if len(sys.argv) > 2 and sys.argv[2] == "concurrent":
+        return concurrent(nexr)
     # (datatype, op, K, M, n, pinned mask over [srcs..., dsts...], in place on src0)
     cases = [(mg.F32, mg.SUM, 2, 1, 3_000_017, 0, False), (mg.BF16, mg.SUM, 8, 1, 1_000_003, 0, False),
              (mg.I8, mg.MINMAX, 4, 2, 2_000_001, 0b000010, False), (mg.F16, mg.PROD, 3, 1, 777_777, 0b0101, False),

@@ -29,3 +29,11 @@ def test_host_path_matches_oracle(path):
     p = subprocess.run([sys.executable, os.path.join(HERE, "host_path_worker.py"), path], capture_output=True,
                        text=True, timeout=300, env=env)
     assert p.returncode == 0 and "host-path ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+
+
+@pytest.mark.parametrize("path", ["chunk-pipeline", "copy-team-3"])
+def test_host_path_concurrent_callers(path):
+    env = dict(os.environ, **PATHS[path])
+    p = subprocess.run([sys.executable, os.path.join(HERE, "host_path_worker.py"), path, "concurrent"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0 and "host-path ok concurrent" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
