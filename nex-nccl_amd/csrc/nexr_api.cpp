@@ -627,7 +627,16 @@ nexrResult_t reduceCopyHostTeam(int nSrcs, const void* const* srcs, const bool* 
                                 int datatype, int op, uint64_t redOpArg, int nPreOpSrcs, const uint64_t* preOpArgs,
                                 int postOp, hipStream_t s, int nThreads) {
   const size_t esz = typeSize(datatype);
-  static const long chunkOverride = envLong("NEXR_HOST_MT_CHUNK_BYTES", 32l << 20);
+  // A team's chunk is an eighth of a buffer, between 4 MiB and NEXR_HOST_MT_CHUNK_BYTES (32 MiB), so
+  // that a call runs at least 8 chunks through the 3 slots; alone, NEXR_HOST_SMALL_CHUNK_BYTES (4 MiB).
+  static const long chunkTeam = envLong("NEXR_HOST_MT_CHUNK_BYTES", 32l << 20);
+  static const long chunkSolo = envLong("NEXR_HOST_SMALL_CHUNK_BYTES", 4l << 20);
+  long chunkOverride = chunkSolo;
+  if (nThreads > 1) {
+    const long eighth = (long)(nElts * esz / 8);
+    chunkOverride = eighth < (4l << 20) ? (4l << 20) : eighth;
+    if (chunkOverride > chunkTeam) chunkOverride = chunkTeam;
+  }
   size_t chunkElts = ((size_t)(chunkOverride > 4096 ? chunkOverride : 4096) / esz) & ~(size_t)15;
   if (chunkElts > nElts) chunkElts = nElts;
   const size_t chunkBytes = ((chunkElts * esz) + 4095) & ~(size_t)4095;
@@ -837,12 +846,21 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
     return nexrSuccess;
   }
   const size_t esz = typeSize(datatype);
-  // Large calls: the CPU copy team into pinned zero-copy slots (reduceCopyHostTeam).
-  static const long mtMin = envLong("NEXR_HOST_MT_MIN_BYTES", 32l << 20);
+  // Pageable buffers, by the pageable bytes the call moves (profiles/r02_host_sizes_sweep.log):
+  //   <= NEXR_HOST_SOLO_MAX_BYTES (4 MiB; the emulated ring's slices): the calling thread copies them
+  //      into pinned zero-copy slots (reduceCopyHostTeam, one thread): 1.2-1.9x the runtime copies;
+  //   >= NEXR_HOST_MT_MIN_BYTES (256 MiB): a team of NEXR_HOST_COPY_THREADS (8) threads does: 1.1-1.2x;
+  //   in between, and always with NEXR_HOST_COPY_THREADS=0: the runtime-copy chunk pipeline below,
+  //      which is as fast or faster there.
+  static const long mtMin = envLong("NEXR_HOST_MT_MIN_BYTES", 256l << 20);
+  static const long soloMax = envLong("NEXR_HOST_SOLO_MAX_BYTES", 4l << 20);
   static const long mtThreads = envLong("NEXR_HOST_COPY_THREADS", 8);
-  if (mtThreads > 1 && (uint64_t)(nSrcs + nDsts - nPinned) * nElts * esz >= (uint64_t)mtMin)
+  const uint64_t pageable = (uint64_t)(nSrcs + nDsts - nPinned) * nElts * esz;
+  if (mtThreads >= 1 && (pageable >= (uint64_t)mtMin || pageable <= (uint64_t)soloMax)) {
+    const bool large = pageable >= (uint64_t)mtMin;
     return reduceCopyHostTeam(nSrcs, srcs, psrc, zsrc, nDsts, dsts, pdst, zdst, nElts, datatype, devRedOp, redOpArg,
-                              nPreOpSrcs, preOpArgs, postOp, s, (int)(mtThreads > 64 ? 64 : mtThreads));
+                              nPreOpSrcs, preOpArgs, postOp, s, large ? (int)(mtThreads > 64 ? 64 : mtThreads) : 1);
+  }
   // Some buffers pageable: a two-stream chunk pipeline through device memory for those only; the
   // pinned ones (e.g. the emulated transport's FIFOs) are read and written in place by the kernel.
   static const long chunkOverride = envLong("NEXR_HOST_CHUNK_BYTES", 8l << 20);
