@@ -494,8 +494,9 @@ def h2d_inclusive(pkg, cfg, reps: int = 3):
             "path": "nexrReduceCopyHost, pinned host buffers: zero-copy kernel over PCIe Gen5 x16",
             "pageable": {"value": round(alg / t_page / 1e9, 2), "ms_per_call": round(t_page * 1e3, 3),
                          "path": "host copy team (8 threads) into pinned zero-copy slots, 32 MiB chunks, "
-                                 "kernel over PCIe, copy team out (calls under 32 MiB: the runtime's "
-                                 "H2D -> kernel -> D2H two-stream chunk pipeline)"}}
+                                 "kernel over PCIe, copy team out (the path for calls of 256 MiB or more; "
+                                 "4-256 MiB: runtime H2D -> kernel -> D2H chunk pipeline; up to 4 MiB: the "
+                                 "calling thread's copies into zero-copy slots)"}}
 
 
 # ---- the two ways to drive N GPUs ---------------------------------------------------------------
