@@ -293,7 +293,7 @@ def c1_ring(iters: int = 20) -> dict:
     x = [rng.integers(-1000, 1000, count).astype(np.float32) for _ in range(n)]
     expect = x[0] + x[1]
     ol = oracle.lib()
-    cpu_fn = ctypes.cast(ol.oracle_reduce_copy_fn, ctypes.c_void_p).value
+    cpu_fn = ctypes.cast(ol.oracle_reduce_copy_emulated_fn, ctypes.c_void_p).value
     out = {"workload": "fp32 sum all-reduce, 4 MiB per rank, 2 emulated ranks, ring SIMPLE, 1 channel"}
     for name, mode, fn in (("device", ring.DEVICE_MEMORY, None), ("host_staged", ring.HOST_MEMORY, None),
                            ("cpu_oracle", ring.HOST_MEMORY, cpu_fn)):
@@ -319,7 +319,8 @@ def c1_ring(iters: int = 20) -> dict:
         out[name] = {"ms_per_call": round(dt * 1e3, 3), "algbw_gbs": round(count * 4 / dt / 1e9, 2), "calls": reps,
                      "exact": all(np.array_equal(g, expect) for g in got)}
     out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); cpu_oracle runs the same schedule with the "
-                   "C restatement as its reduce-copy on host cores")
+                   "reference's CPU execution of reduceCopy (oracle_reduce_copy_emulated_fn: 480 emulated threads, "
+                   "Unroll 4) as its reduce-copy on host cores")
     return out
 
 
@@ -353,17 +354,25 @@ def cpu_sample(cfg, n: int, seed: int = 7):
     return srcs, dsts
 
 
-def cpu_baseline(cfg, seconds: float = 10.0, threads: int = 1, sample=None):
+# The reference's geometry for a ring step's reduceCopy in the fork's g++ build (oracle/nexr_oracle.c,
+# oracle_reduce_copy_emulated_fn): 480 worker threads (prims_simple.h:614), Unroll 4 (device.h:1131-1134).
+REF_EXECUTION = (480, 4)
+
+
+def cpu_baseline(cfg, seconds: float = 10.0, threads: int = 1, sample=None, emulated=REF_EXECUTION):
     """The C oracle over the FULL configuration (every buffer at cfg['buf_bytes']) for about
-    `seconds`: returns (GB/s of algorithmic bytes, calls, seconds)."""
+    `seconds`: returns (GB/s of algorithmic bytes, calls, seconds). `emulated` = (threads, unroll)
+    runs the reference's own CPU execution of reduceCopy (cooperative emulated threads one after
+    another over reduceCopyPacks' hunk layout); None runs the plain element loop."""
     import oracle
 
     n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
     srcs, dsts = sample if sample is not None else cpu_sample(cfg, n)
-    oracle.reduce_copy(srcs, cfg["m"], cfg["dt"], cfg["op"], cfg["arg"], dsts=dsts, threads=threads)  # warm
+    kw = dict(dsts=dsts, threads=threads, emulated=emulated)
+    oracle.reduce_copy(srcs, cfg["m"], cfg["dt"], cfg["op"], cfg["arg"], **kw)  # warm
     reps, t0 = 0, time.perf_counter()
     while True:
-        oracle.reduce_copy(srcs, cfg["m"], cfg["dt"], cfg["op"], cfg["arg"], dsts=dsts, threads=threads)
+        oracle.reduce_copy(srcs, cfg["m"], cfg["dt"], cfg["op"], cfg["arg"], **kw)
         reps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -389,15 +398,27 @@ def cpu_baseline_entry(cfg, seconds: float) -> dict:
     gbs1, reps1, el1 = cpu_baseline(cfg, seconds, threads=1, sample=sample)
     nthreads, how = usable_cores()
     gbsN, repsN, elN = cpu_baseline(cfg, max(2.0, seconds / 4), threads=nthreads, sample=sample)
+    lp1, lreps1, lel1 = cpu_baseline(cfg, max(2.0, seconds / 3), threads=1, sample=sample, emulated=None)
+    lpN, lrepsN, lelN = cpu_baseline(cfg, max(1.0, seconds / 6), threads=nthreads, sample=sample, emulated=None)
     mib = cfg["buf_bytes"] >> 20
+    w, u = REF_EXECUTION
     return {"value": round(gbs1, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"the full benchmarked call: {cfg['k']} x {mib} MiB in, {cfg['m']} x {mib} MiB out "
                       f"({cfg['workload']}), {reps1} calls in {el1:.1f} s on 1 thread of {cpu_model()}",
-            "note": "times oracle/nexr_oracle.c, the build's C restatement of reduceCopy (one thread = the "
-                    "reference emulator, which runs a launch's fibers on one pthread); the compiled reference "
-                    f"reduceCopy itself ran at {REF_CPU_GBS_SURVEY} GB/s on one core in the survey (SURVEY §6)",
+            "note": f"times oracle_reduce_copy_emulated (oracle/nexr_oracle.c): the reference's CPU execution of "
+                    f"reduceCopy restated — {w} emulated threads (a ring step's workers) run one after another on "
+                    f"one pthread, as the fork's emulator runs a launch's fibers, each over reduceCopyPacks' hunk "
+                    f"layout with Unroll {u} and a memcpy per pack; the compiled reference reduceCopy ran at "
+                    f"{REF_CPU_GBS_SURVEY} GB/s on one core of the survey's container (SURVEY §6)",
             "all_cores": {"value": round(gbsN, 3), "cores": nthreads, "cores_from": how,
-                          "sample": f"{repsN} calls in {elN:.1f} s, one pthread per contiguous slice"}}
+                          "sample": f"{repsN} calls in {elN:.1f} s, one emulated launch per pthread on a "
+                                    f"contiguous slice"},
+            "element_loop": {"value": round(lp1, 3), "cores": 1, "all_cores_value": round(lpN, 3),
+                             "all_cores": nthreads,
+                             "sample": f"{lreps1} calls in {lel1:.1f} s on 1 thread, {lrepsN} calls in "
+                                       f"{lelN:.1f} s on {nthreads}",
+                             "note": "the same arithmetic as a plain per-element loop (oracle_reduce_copy): what "
+                                     "a straightforward CPU implementation reaches, not the reference's path"}}
 
 
 # ---- N > 1: the C5 summary ----------------------------------------------------------------------

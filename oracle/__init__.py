@@ -35,6 +35,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_reduce_copy.restype = i32
         L.oracle_reduce_copy_mt.argtypes = [i32, P(vp), i32, P(vp), sz, i32, i32, u64, i32, P(u64), i32, i32]
         L.oracle_reduce_copy_mt.restype = i32
+        L.oracle_reduce_copy_emulated.argtypes = [i32, P(vp), i32, P(vp), sz, i32, i32, u64, i32, P(u64), i32, i32, i32]
+        L.oracle_reduce_copy_emulated.restype = i32
+        L.oracle_reduce_copy_emulated_mt.argtypes = [i32, P(vp), i32, P(vp), sz, i32, i32, u64, i32, P(u64), i32,
+                                                     i32, i32, i32]
+        L.oracle_reduce_copy_emulated_mt.restype = i32
         L.oracle_host_to_dev_redop.argtypes = [i32, i32, i32, P(u64)]
         L.oracle_host_to_dev_redop.restype = i32
         L.oracle_onerank_reference_coverage.argtypes = [sz, i32]
@@ -60,8 +65,12 @@ def _ptrs(arrs):
 
 def reduce_copy(srcs: Sequence[np.ndarray], n_dsts: int, datatype: int, dev_red_op: int, red_op_arg: int = 0,
                 pre_op_args: Optional[Sequence[int]] = None, post_op: bool = False, threads: int = 1,
-                dsts: Optional[Sequence[np.ndarray]] = None) -> list:
-    """Run the oracle on numpy buffers (any dtype view; the bytes are what count). Returns dsts."""
+                dsts: Optional[Sequence[np.ndarray]] = None, emulated: Optional[tuple] = None) -> list:
+    """Run the oracle on numpy buffers (any dtype view; the bytes are what count). Returns dsts.
+
+    ``emulated=(n_threads, unroll)`` runs the reference's CPU execution of reduceCopy instead of the
+    element loop: that many cooperative emulated threads, one after another, over reduceCopyPacks'
+    hunk layout (``oracle_reduce_copy_emulated``; ``threads`` > 1 gives each pthread a slice)."""
     srcs = [np.ascontiguousarray(s) for s in srcs]
     n_bytes = srcs[0].nbytes
     esz = lib().oracle_type_size(int(datatype))
@@ -74,7 +83,13 @@ def reduce_copy(srcs: Sequence[np.ndarray], n_dsts: int, datatype: int, dev_red_
     pre_arr = (ctypes.c_uint64 * len(pre))(*[int(v) & 0xFFFFFFFFFFFFFFFF for v in pre]) if pre else None
     args = [len(srcs), _ptrs(srcs), len(dsts), _ptrs(dsts), n, int(datatype), int(dev_red_op),
             int(red_op_arg) & 0xFFFFFFFFFFFFFFFF, len(pre), pre_arr, 1 if post_op else 0]
-    if threads > 1:
+    if emulated is not None:
+        nt, unroll = int(emulated[0]), int(emulated[1])
+        if threads > 1:
+            rc = lib().oracle_reduce_copy_emulated_mt(*args, nt, unroll, int(threads))
+        else:
+            rc = lib().oracle_reduce_copy_emulated(*args, nt, unroll)
+    elif threads > 1:
         rc = lib().oracle_reduce_copy_mt(*args, int(threads))
     else:
         rc = lib().oracle_reduce_copy(*args)

@@ -315,6 +315,204 @@ int oracle_reduce_copy_mt(int nSrcs, const void* const* srcs, int nDsts, void* c
   return R_OK;
 }
 
+/* ---- the reference's CPU execution of reduceCopy: cooperative threads run one after another ----
+ *
+ * The fork runs a kernel launch's threads as fibers of ONE pthread (cuda_emulator.hh:342-382), and
+ * reduceCopy has no barrier, so every emulated thread runs its whole reduceCopy before the next one
+ * starts. oracle_reduce_copy_emulated restates that execution, not just the element arithmetic:
+ * nThreads threads of 32-lane warps, each running reduceCopy's pass sequence (common_kernel.h:
+ * 288-328: 16-B packs with Unroll, then Unroll = 1, when every pointer is 16-B aligned; then
+ * sizeof(T) packs with Unroll*(16/sizeof(T))/2, then Unroll = 1) over reduceCopyPacks' hunk layout
+ * (:92-113: thread start warp*Unroll*32*BPP + lane*BPP, stride nWarps hunks, partial hunks only
+ * at Unroll = 1, the warp rotation at the end of every pass :255-265), with every pack moved by a
+ * BPP-byte memcpy (the fork's global_memcpy, op128.h:165-179) into a register pack and folded
+ * element by element. The result equals the element loop's; the cost is the reference's (strided
+ * 16-B accesses, each 64-B line visited by four emulated threads a whole sweep apart). bench.py
+ * times it as the reference CPU path. */
+typedef struct {
+  int nSrcs, nDsts, dt, nPreOp, postOp, nThreads, unroll;
+  const char* const* srcs;
+  char* const* dsts;
+  const uint64_t* pre;
+  Fn fn;
+} EJob;
+
+/* One reduceCopyPacks pass of one emulated thread (common_kernel.h:87-266). */
+#define EMU_PASS(NAME, T, BPP, PREOP, REDUCE, POSTOP)                                              \
+  static void NAME(const EJob* j, int Unroll, int* thread, int64_t* nBehind, int64_t* nAhead) {     \
+    const Fn fn = j->fn;                                                                            \
+    const int isPreMul = fn.op == OP_PREMULSUM, isPostDiv = fn.op == OP_SUMPOSTDIV;                \
+    const int64_t hunk = (int64_t)Unroll * 32 * BPP;                                                \
+    const int nWarps = j->nThreads / 32, warp = *thread / 32, lane = *thread % 32;                  \
+    int64_t tBehind = *nBehind + warp * hunk + lane * BPP;                                         \
+    int64_t tAhead = *nAhead - (warp * hunk + lane * BPP);                                         \
+    int64_t nHunks = *nAhead / hunk;                                                                \
+    *nBehind += nHunks * hunk;                                                                      \
+    *nAhead -= nHunks * hunk;                                                                       \
+    if (Unroll == 1 && BPP <= *nAhead) {                                                            \
+      nHunks += 1;                                                                                  \
+      *nBehind += *nAhead - *nAhead % BPP;                                                          \
+      *nAhead = *nAhead % BPP;                                                                      \
+    }                                                                                               \
+    nHunks -= warp;                                                                                 \
+    const int epp = BPP / (int)sizeof(T);                                                           \
+    while (Unroll == 1 ? (BPP <= tAhead) : (0 < nHunks)) {                                          \
+      T acc[128], tmp[16 / sizeof(T)]; /* Unroll packs of epp elements: at most 8 x 16 B */         \
+      for (int u = 0; u < Unroll; u++) {                                                            \
+        memcpy(&acc[u * epp], j->srcs[0] + tBehind + (int64_t)u * 32 * BPP, (size_t)BPP);           \
+        if (isPreMul && 0 < j->nPreOp)                                                              \
+          for (int e = 0; e < epp; e++) acc[u * epp + e] = PREOP(acc[u * epp + e], 0);              \
+      }                                                                                             \
+      for (int s = 1; s < j->nSrcs; s++)                                                            \
+        for (int u = 0; u < Unroll; u++) {                                                          \
+          memcpy(tmp, j->srcs[s] + tBehind + (int64_t)u * 32 * BPP, (size_t)BPP);                   \
+          for (int e = 0; e < epp; e++) {                                                           \
+            T v = tmp[e];                                                                           \
+            if (isPreMul && s < j->nPreOp) v = PREOP(v, s);                                         \
+            acc[u * epp + e] = REDUCE(&fn, acc[u * epp + e], v);                                    \
+          }                                                                                         \
+        }                                                                                           \
+      if (isPostDiv && j->postOp)                                                                   \
+        for (int u = 0; u < Unroll; u++)                                                            \
+          for (int e = 0; e < epp; e++) acc[u * epp + e] = POSTOP(&fn, acc[u * epp + e]);           \
+      for (int d = 0; d < j->nDsts; d++)                                                            \
+        for (int u = 0; u < Unroll; u++)                                                            \
+          memcpy(j->dsts[d] + tBehind + (int64_t)u * 32 * BPP, &acc[u * epp], (size_t)BPP);         \
+      tBehind += nWarps * hunk;                                                                     \
+      tAhead -= nWarps * hunk;                                                                      \
+      nHunks -= nWarps;                                                                             \
+    }                                                                                               \
+    if (Unroll == 1 && nHunks > 0) nHunks -= nWarps;                                                \
+    *thread = (int)(-nHunks) * 32 + lane; /* warp rotation, :262-265 */                            \
+  }
+
+/* (PRE_* are run_job's pre-op macros above). Pack sizes are compile-time, as in the reference's
+ * templates: BytePack<16> and BytePack<sizeof(T)>. */
+#define EMU_TYPE(SFX, T, PREOP, REDUCE, POSTOP)                       \
+  EMU_PASS(emu_pass16_##SFX, T, 16, PREOP, REDUCE, POSTOP)            \
+  EMU_PASS(emu_passT_##SFX, T, (int)sizeof(T), PREOP, REDUCE, POSTOP)
+EMU_TYPE(i8, uint8_t, PRE_U8, red_uint8_t_1, div_u8)
+EMU_TYPE(u8, uint8_t, PRE_U8, red_uint8_t_0, div_u8)
+EMU_TYPE(i32, uint32_t, PRE_U32, red_uint32_t_1, div_u32)
+EMU_TYPE(u32, uint32_t, PRE_U32, red_uint32_t_0, div_u32)
+EMU_TYPE(i64, uint64_t, PRE_U64, red_uint64_t_1, div_u64)
+EMU_TYPE(u64, uint64_t, PRE_U64, red_uint64_t_0, div_u64)
+EMU_TYPE(f32, float, PRE_F32, red_f32, NOPOST)
+EMU_TYPE(f64, double, PRE_F64, red_f64, NOPOST)
+EMU_TYPE(f16, uint16_t, PRE_F16, red_f16, NOPOST)
+EMU_TYPE(bf16, uint16_t, PRE_BF16, red_bf16, NOPOST)
+
+typedef void (*EmuPassFn)(const EJob*, int, int*, int64_t*, int64_t*);
+
+/* reduceCopy for one emulated thread (common_kernel.h:273-329). */
+static void emu_thread(const EJob* j, EmuPassFn pass16, EmuPassFn passT, int tid, int64_t nBytes, int aligned16) {
+  const int esz = (int)oracle_type_size(j->dt);
+  int thread = tid;
+  int64_t nBehind = 0, nAhead = nBytes;
+  if (16 > esz && aligned16) {
+    pass16(j, j->unroll, &thread, &nBehind, &nAhead);
+    if (nAhead == 0) return;
+    pass16(j, 1, &thread, &nBehind, &nAhead);
+    if (nAhead == 0) return;
+  }
+  passT(j, j->unroll * (16 / esz) / 2, &thread, &nBehind, &nAhead);
+  if (nAhead == 0) return;
+  passT(j, 1, &thread, &nBehind, &nAhead);
+}
+
+/* nThreads (a multiple of 32, at most 1024) emulated threads with reduceCopy's Unroll (the fork's
+ * ring steps: 512 threads, COLL_UNROLL 4), run one after another on the calling thread. */
+int oracle_reduce_copy_emulated(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                                int datatype, int devRedOp, uint64_t redOpArg, int nPreOpSrcs,
+                                const uint64_t* preOpArgs, int postOp, int nThreads, int unroll) {
+  int r = check(nSrcs, nDsts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != R_OK) return r;
+  if (nThreads < 32 || nThreads > 1024 || nThreads % 32 || unroll < 1 || unroll > 8) return R_INVALID;
+  if (nDsts == 0 || nElts == 0) return R_OK; /* :288-289 */
+  EJob j = {nSrcs, nDsts, datatype, nPreOpSrcs, postOp, nThreads, unroll, (const char* const*)srcs,
+            (char* const*)dsts, preOpArgs, {0, 0, 0, 0}};
+  make_fn(&j.fn, devRedOp, redOpArg);
+  static const EmuPassFn p16[DT_NUM] = {emu_pass16_i8, emu_pass16_u8, emu_pass16_i32, emu_pass16_u32,
+                                       emu_pass16_i64, emu_pass16_u64, emu_pass16_f16, emu_pass16_f32,
+                                       emu_pass16_f64, emu_pass16_bf16, NULL, NULL};
+  static const EmuPassFn pT[DT_NUM] = {emu_passT_i8, emu_passT_u8, emu_passT_i32, emu_passT_u32,
+                                      emu_passT_i64, emu_passT_u64, emu_passT_f16, emu_passT_f32,
+                                      emu_passT_f64, emu_passT_bf16, NULL, NULL};
+  int aligned = 1; /* the __all_sync vote over every src and dst pointer, :299-303 */
+  for (int s = 0; s < nSrcs; s++) aligned &= ((uintptr_t)srcs[s] % 16) == 0;
+  for (int d = 0; d < nDsts; d++) aligned &= ((uintptr_t)dsts[d] % 16) == 0;
+  const int64_t nBytes = (int64_t)(nElts * oracle_type_size(datatype));
+  for (int t = 0; t < nThreads; t++) emu_thread(&j, p16[datatype], pT[datatype], t, nBytes, aligned);
+  return R_OK;
+}
+
+/* The reference's geometry for a ring step's reduceCopy in the fork's g++ build: NCCL_CUDA_ARCH is
+ * 0 without nvcc, so Unroll = ncclCollUnroll() = 4 (device.h:652-655, :1131-1134), and a SIMPLE
+ * step of NCCL_SIMPLE_MAX_NTHREADS = 512 threads with a send peer gives nworkers = 512 - 32 = 480
+ * (prims_simple.h:614, device.h:715-716). With the nexrReduceCopyFn signature (include/nexr_ring.h),
+ * so the emulated collectives can run every step the reference's way on a host core. */
+enum { REF_RING_WORKERS = 480, REF_COLL_UNROLL = 4 };
+int oracle_reduce_copy_emulated_fn(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                                   int datatype, int devRedOp, uint64_t redOpArg, int nPreOpSrcs,
+                                   const uint64_t* preOpArgs, int postOp, void* stream) {
+  (void)stream;
+  return oracle_reduce_copy_emulated(nSrcs, srcs, nDsts, dsts, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs,
+                                     preOpArgs, postOp, REF_RING_WORKERS, REF_COLL_UNROLL);
+}
+
+typedef struct {
+  int nSrcs, nDsts, dt, op, nPreOp, postOp, nThreads, unroll, ret;
+  const void* srcs[8];
+  void* dsts[8];
+  const uint64_t* pre;
+  uint64_t arg;
+  size_t nElts;
+} EmuSlice;
+
+static void* emu_slice_main(void* a) {
+  EmuSlice* s = (EmuSlice*)a;
+  s->ret = oracle_reduce_copy_emulated(s->nSrcs, s->srcs, s->nDsts, s->dsts, s->nElts, s->dt, s->op, s->arg,
+                                       s->nPreOp, s->pre, s->postOp, s->nThreads, s->unroll);
+  return NULL;
+}
+
+/* The same over nPthreads contiguous slices, one emulated launch per pthread (as separate blocks
+ * of a launch would run on separate host threads) — the "all cores" reference CPU path. Slices
+ * start at 4 KiB multiples, so each keeps the call's pointer alignment. */
+int oracle_reduce_copy_emulated_mt(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts, size_t nElts,
+                                   int datatype, int devRedOp, uint64_t redOpArg, int nPreOpSrcs,
+                                   const uint64_t* preOpArgs, int postOp, int nThreads, int unroll, int nPthreads) {
+  int r = check(nSrcs, nDsts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
+  if (r != R_OK) return r;
+  if (nPthreads < 1) nPthreads = 1;
+  if (nPthreads > 256) nPthreads = 256;
+  const size_t esz = oracle_type_size(datatype);
+  size_t per = (nElts + (size_t)nPthreads - 1) / (size_t)nPthreads;
+  per = (per + 4096 / esz - 1) / (4096 / esz) * (4096 / esz);
+  pthread_t th[256];
+  int live[256];
+  EmuSlice sl[256];
+  for (int t = 0; t < nPthreads; t++) {
+    size_t b = per * (size_t)t, e = b + per;
+    live[t] = 0;
+    if (b >= nElts) continue;
+    if (e > nElts) e = nElts;
+    EmuSlice* s = &sl[t];
+    s->nSrcs = nSrcs; s->nDsts = nDsts; s->dt = datatype; s->op = devRedOp; s->nPreOp = nPreOpSrcs;
+    s->postOp = postOp; s->nThreads = nThreads; s->unroll = unroll; s->pre = preOpArgs; s->arg = redOpArg;
+    s->nElts = e - b; s->ret = R_OK;
+    for (int k = 0; k < nSrcs; k++) s->srcs[k] = (const char*)srcs[k] + b * esz;
+    for (int d = 0; d < nDsts; d++) s->dsts[d] = (char*)dsts[d] + b * esz;
+    if (pthread_create(&th[t], NULL, emu_slice_main, s) == 0) live[t] = 1;
+    else emu_slice_main(s);
+  }
+  for (int t = 0; t < nPthreads; t++)
+    if (live[t]) pthread_join(th[t], NULL);
+  for (int t = 0; t < nPthreads; t++)
+    if ((size_t)t * per < nElts && sl[t].ret != R_OK) return sl[t].ret;
+  return R_OK;
+}
+
 /* ---- LL protocol step (reference src/device/prims_ll.h:218-283) ------------------------------ */
 /* One element through one reduce step with the PEER as the first operand: out = op(c, v). */
 static void elem_reduce(int dt, const Fn* fn, const uint8_t* c, const uint8_t* v, uint8_t* out) {

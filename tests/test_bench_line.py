@@ -131,8 +131,10 @@ def test_cpu_baseline_runs_the_full_configuration(monkeypatch):
     seen = {}
     import oracle
 
-    def fake_rc(srcs, m, dt, op, arg, dsts=None, threads=1):
+    def fake_rc(srcs, m, dt, op, arg, dsts=None, threads=1, emulated=None):
         seen.setdefault("n", srcs[0].size)
+        seen.setdefault("first", (threads, emulated))
+        seen.setdefault("modes", set()).add((threads > 1, emulated))
         seen["threads"] = threads
         return dsts
 
@@ -144,3 +146,8 @@ def test_cpu_baseline_runs_the_full_configuration(monkeypatch):
     assert e["cores"] == 1 and e["kind"] == "port" and "1 MiB" in e["sample"]
     assert e["all_cores"]["cores"] == bench.usable_cores()[0] == seen["threads"]
     assert "1.79" in e["note"]
+    # the headline is the reference's execution (480 emulated threads, Unroll 4) on one core; the
+    # plain element loop is reported beside it, both on 1 and on all cores
+    assert seen["first"] == (1, (480, 4))
+    assert seen["modes"] == {(False, (480, 4)), (True, (480, 4)), (False, None), (True, None)}
+    assert e["element_loop"]["cores"] == 1 and e["element_loop"]["all_cores"] == bench.usable_cores()[0]

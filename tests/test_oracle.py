@@ -165,3 +165,60 @@ def test_onerank_reference_coverage(oracle):
     assert oracle.onerank_reference_coverage(131073, mg.F32) == 131072
     assert oracle.onerank_reference_coverage(4096, mg.F32) == 4096
     assert oracle.onerank_reference_coverage(100, mg.F32) == 100
+
+
+# ---- the reference's CPU execution of reduceCopy (oracle_reduce_copy_emulated) ----------------------
+# bench.py times it as the reference CPU path, so it must compute exactly what the element loop does
+# for every geometry the reference can run it with: the golden vectors, unaligned pointers (the
+# sizeof(T)-pack passes), guard bytes around every destination (the hunk layout and the warp
+# rotation between passes cover each element exactly once), and the pthread-sliced variant.
+
+@pytest.mark.parametrize("geom", [(512, 4), (64, 1), (96, 2), (1024, 8)])
+def test_emulated_execution_matches_every_golden_vector(oracle, golden_cases, geom):
+    cases = golden_cases if geom == (512, 4) else golden_cases[::7]
+    bad = []
+    for c in cases:
+        srcs = mg.gen_inputs(c["dt"], c["k"], c["n"], c["seed"], c["special"])
+        (out,) = oracle.reduce_copy(srcs, 1, c["dt"], c["op"], c["arg"], c["pre"], c["post"], emulated=geom)
+        if hashlib.sha256(mg.canon_bytes(c["dt"], out)).hexdigest() != c["sha256"]:
+            bad.append((c["name"], mg.DT_NAMES[c["dt"]], c["k"], c["n"]))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
+
+
+@pytest.mark.parametrize("dt", sorted(mg.DT_NAMES))
+def test_emulated_execution_unaligned_and_guarded(oracle, dt):
+    rng = np.random.default_rng(40 + dt)
+    esz = oracle.lib().oracle_type_size(dt)
+    for n in (1, 5, 33, 1000, 40_961):
+        for offs in ((0, 0, 0), (esz, esz, esz), (0, esz, 0), (3 * esz, 0, 5 * esz)):
+            k, m = 2, 2
+            raw = [rng.integers(0, 256, (n + 16) * esz + 64, dtype=np.uint8) for _ in range(k)]
+            srcs = [r[offs[i] if i < 2 else 0:][: n * esz] for i, r in enumerate(raw)]
+            srcs = [s.view(np.uint8) for s in srcs]
+            exp = oracle.reduce_copy(srcs, m, dt, mg.SUM)
+            outs = []
+            for d in range(m):
+                buf = np.full(n * esz + 128, 0xA5, dtype=np.uint8)
+                o = buf[64 + (offs[2] if d == 0 else 0):][: n * esz]
+                outs.append((buf, o))
+            oracle.reduce_copy(srcs, m, dt, mg.SUM, dsts=[o for _, o in outs], emulated=(512, 4))
+            for (buf, o), e in zip(outs, exp):
+                assert o.tobytes() == e.tobytes(), (dt, n, offs)
+                lo = 64 + (offs[2] if o is outs[0][1] else 0)
+                assert (buf[:lo] == 0xA5).all() and (buf[lo + n * esz:] == 0xA5).all(), (dt, n, offs, "guard")
+
+
+def test_emulated_execution_sliced_over_pthreads(oracle):
+    srcs = mg.gen_inputs(mg.F32, 3, 1_000_003, 99, special=True)
+    one = oracle.reduce_copy(srcs, 2, mg.F32, mg.SUM, emulated=(512, 4))
+    many = oracle.reduce_copy(srcs, 2, mg.F32, mg.SUM, emulated=(512, 4), threads=5)
+    loop = oracle.reduce_copy(srcs, 2, mg.F32, mg.SUM)
+    for a, b, c in zip(one, many, loop):
+        assert mg.canon_bytes(mg.F32, a) == mg.canon_bytes(mg.F32, b) == mg.canon_bytes(mg.F32, c)
+
+
+def test_emulated_execution_rejects_bad_geometry(oracle):
+    a = np.zeros(64, np.float32)
+    for geom in ((0, 4), (100, 4), (2048, 4), (512, 0), (512, 9)):
+        with pytest.raises(ValueError):
+            oracle.reduce_copy([a, a], 1, mg.F32, mg.SUM, emulated=geom)

@@ -151,3 +151,20 @@ def test_ll128_ring_matches_peer_first_fold_oracle(ring, oracle, oracle_ll128_fn
     exp = ring_allreduce_expected_ll(inputs, dt, op, buff, proto="ll128")
     for r in range(n_ranks):
         assert mg.canon_bytes(dt, recv[r]) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3])
+@pytest.mark.parametrize("dt,op,special", CASES[:5])
+def test_ring_with_reference_execution_steps(ring, oracle, n_ranks, dt, op, special):
+    """bench.py's C1 CPU leg: every step served by the reference's CPU execution of reduceCopy
+    (oracle_reduce_copy_emulated_fn, 480 emulated threads, Unroll 4) — same results as the fold-order
+    restatement, including steps whose FIFO slots are not 16-B aligned to the user buffers."""
+    from oracle.ring import ring_allreduce_expected
+    fn = ctypes.cast(oracle.lib().oracle_reduce_copy_emulated_fn, ctypes.c_void_p).value
+    buff = 64 << 10
+    count = 30_000 + 5 * n_ranks + 1
+    inputs = mg.gen_inputs(dt, n_ranks, count, 0xE1 + dt + op, special)
+    got = _run(ring, fn, inputs, dt, op, buff)
+    exp = ring_allreduce_expected(inputs, dt, op, buff)
+    for r in range(n_ranks):
+        assert mg.canon_bytes(dt, got[r]) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
