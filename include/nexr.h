@@ -14,8 +14,9 @@
  *   - the caller owns every buffer; nothing is allocated or freed inside a hot call;
  *   - device calls are stream-ordered and asynchronous on the given HIP stream (NULL = the
  *     default stream of the current device); they never synchronise the host;
- *   - calls are safe concurrently on different devices / streams (no global mutable state: tuning
- *     knobs are read from the environment once; host staging resources are per thread and device);
+ *   - calls are safe concurrently on different devices / streams (no global mutable state apart
+ *     from the process-wide reduction semantics below, set before the first call: tuning knobs are
+ *     read from the environment once; host staging resources are pooled per device);
  *   - errors are returned, never aborted on.
  */
 #ifndef NEXR_H_
@@ -248,6 +249,35 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
                                           const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
                                           uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
                                           nexrStream_t stream);
+
+/*
+ * Reduction semantics — which nex-nccl the library reproduces bit for bit. Process-wide, like an
+ * NCCL parameter: the initial value comes from NEXR_SEMANTICS ("nccl", "fork" or "shipped"; default
+ * "nccl"); nexrSetSemantics changes it for every later call (set it before the first call that
+ * matters; calls already queued keep theirs). It applies to nexrReduceCopy, nexrReduceCopyBatch,
+ * nexrReduceCopyMultiDevice, nexrReduceCopyHost, nexrLaunchOneRank, nexrReduceCopyLL and
+ * nexrReduceCopyLL128, and so to every emulated collective built on them (include/nexr_ring.h).
+ *   nexrSemanticsNccl     real arithmetic; Min/Max compared at the signedness of `datatype`
+ *                         (upstream NCCL). The default.
+ *   nexrSemanticsFork     the fork with SKIP_COMP removed: real arithmetic under the fork's own kernel
+ *                         dispatch, where signed-integer Min/Max run on the unsigned kernel
+ *                         (equivalent_primary, src/device/generate.py:128-136) whose FuncMinMax ignores
+ *                         the sign xormask (reduce_kernel.h:59-65), so they compare as unsigned.
+ *   nexrSemanticsShipped  the fork exactly as shipped: `#define SKIP_COMP` (reduce_kernel.h:432) makes
+ *                         every ncclReduceScalar return its FIRST operand and the PreMulSum pre-op and
+ *                         SumPostDiv post-op return their input (:434-539). reduceCopy then copies
+ *                         srcs[0]'s bits to every destination; an LL / LL128 step (peer first) forwards
+ *                         the last peer's data, or src when it has no peer.
+ * Argument validation is the same in every mode.
+ */
+typedef enum {
+  nexrSemanticsNccl = 0,
+  nexrSemanticsFork = 1,
+  nexrSemanticsShipped = 2,
+  nexrNumSemantics = 3
+} nexrSemantics_t;
+NEXR_API nexrResult_t nexrSetSemantics(int semantics);
+NEXR_API nexrResult_t nexrGetSemantics(int* semantics);
 
 /*
  * nexrQueryLaunch — diagnostics: the launch nexrReduceCopy would make for these pointers and this

@@ -70,6 +70,13 @@ class DevRedOp(enum.IntEnum):
     SumPostDiv = 4
 
 
+class Semantics(enum.IntEnum):
+    """nexrSemantics_t (include/nexr.h): which nex-nccl the library reproduces bit for bit."""
+    Nccl = 0     # real arithmetic, min/max at the datatype's signedness (default)
+    Fork = 1     # the fork with SKIP_COMP removed: signed min/max on the unsigned kernel (generate.py:128-136)
+    Shipped = 2  # the fork as shipped: SKIP_COMP (reduce_kernel.h:432), every reduce returns its first operand
+
+
 TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Uint32: 4,
              DataType.Int64: 8, DataType.Uint64: 8, DataType.Float16: 2, DataType.Float32: 4,
              DataType.Float64: 8, DataType.Bfloat16: 2, DataType.Float8e4m3: 1,
@@ -78,7 +85,7 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
                "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrQueryLaunch", "nexrGetPoolStats", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion",
-               "nexrGetLastHipError")
+               "nexrGetLastHipError", "nexrSetSemantics", "nexrGetSemantics")
 
 
 class NexrError(RuntimeError):
@@ -165,6 +172,10 @@ def lib() -> ctypes.CDLL:
     L.nexrQueryLaunch.restype = i32
     L.nexrGetPoolStats.argtypes = [P(u64), P(u64)]
     L.nexrGetPoolStats.restype = i32
+    L.nexrSetSemantics.argtypes = [i32]
+    L.nexrSetSemantics.restype = i32
+    L.nexrGetSemantics.argtypes = [P(i32)]
+    L.nexrGetSemantics.restype = i32
     L.nexrReduceCopyLL.argtypes = [vp, i32, i32, P(vp), P(ctypes.c_uint32), vp, i32, P(vp), P(ctypes.c_uint32), sz,
                                    i32, i32, u64, i32, vp, ctypes.c_uint32, vp]
     L.nexrReduceCopyLL.restype = i32
@@ -280,6 +291,17 @@ def pool_stats() -> tuple:
     a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
     _check(lib().nexrGetPoolStats(ctypes.byref(a), ctypes.byref(b)), "nexrGetPoolStats")
     return a.value, b.value
+
+
+def set_semantics(mode: int) -> None:
+    """nexrSetSemantics: process-wide reduction semantics for every later call (Semantics)."""
+    _check(lib().nexrSetSemantics(int(mode)), "nexrSetSemantics")
+
+
+def get_semantics() -> int:
+    v = ctypes.c_int(-1)
+    _check(lib().nexrGetSemantics(ctypes.byref(v)), "nexrGetSemantics")
+    return v.value
 
 
 def host_to_dev_red_op(op: int, datatype: int, n_ranks: int = 1) -> DevRedOpFull:

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -45,6 +46,67 @@ long envLong(const char* name, long dflt) {
   const char* v = getenv(name);
   if (!v || !*v) return dflt;
   return strtol(v, nullptr, 0);
+}
+
+// Reduction semantics (include/nexr.h, nexrSetSemantics): process-wide, like an NCCL parameter; the
+// initial value comes from NEXR_SEMANTICS the first time a call needs it.
+std::atomic<int> gSemantics{-1};
+
+int semantics() {
+  int s = gSemantics.load(std::memory_order_relaxed);
+  if (s >= 0) return s;
+  const char* v = getenv("NEXR_SEMANTICS");
+  int init = nexrSemanticsNccl;
+  if (v && (!strcmp(v, "fork") || !strcmp(v, "1"))) init = nexrSemanticsFork;
+  if (v && (!strcmp(v, "shipped") || !strcmp(v, "2"))) init = nexrSemanticsShipped;
+  gSemantics.compare_exchange_strong(s, init);
+  return gSemantics.load(std::memory_order_relaxed);
+}
+
+// The fork's kernel dispatch (equivalent_primary, generate.py:128-136): signed Min/Max run on the
+// unsigned kernel, whose FuncMinMax never applies the sign xormask hostToDevRedOp encodes.
+int forkDispatchType(int dt, int op) {
+  if (op != nexrDevMinMax) return dt;
+  switch (dt) {
+    case nexrInt8: return nexrUint8;
+    case nexrInt32: return nexrUint32;
+    case nexrInt64: return nexrUint64;
+  }
+  return dt;
+}
+
+// The parts of a validated SIMPLE call the semantics can change. Shipped (SKIP_COMP): every reduce
+// returns acc = src0, the pre-op and post-op return their input — a K = 1 copy with no arithmetic.
+struct CallShape {
+  int dt, op, nSrcs, nPreOp, postOp;
+  const void* prePtr;
+};
+void applySemantics(CallShape& c) {
+  const int s = semantics();
+  if (s == nexrSemanticsFork) {
+    c.dt = forkDispatchType(c.dt, c.op);
+  } else if (s == nexrSemanticsShipped) {
+    c.op = nexrDevSum;
+    c.nSrcs = 1;
+    c.nPreOp = 0;
+    c.postOp = 0;
+    c.prePtr = nullptr;
+  }
+}
+
+// The same for an LL / LL128 step (after validation): shipped → every reduce returns its first operand,
+// the peer (prims_ll.h:288-294, prims_ll128.h:225-255), with no pre-op and no post-op.
+void llSemantics(int* dt, int* op, int* srcIsInput, int* postOp, int* firstWins) {
+  const int s = semantics();
+  *firstWins = 0;
+  if (s == nexrSemanticsFork) {
+    *dt = forkDispatchType(*dt, *op);
+  } else if (s == nexrSemanticsShipped) {
+    *op = nexrDevSum;
+    *srcIsInput = 0;
+    *postOp = 0;
+    *firstWins = 1;
+  }
 }
 
 // Grid: one workgroup per kTripPacks-pack trip ("one-shot"), capped so that grid x block stays
@@ -185,6 +247,22 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
                               w.preOpArgs);
     if (r != nexrSuccess) return r;
   }
+  std::vector<nexrReduceCopyWork> shaped;  // the works as the semantics run them (applySemantics)
+  if (semantics() != nexrSemanticsNccl && nWorks > 0) {
+    CallShape c0{datatype, op, 1, 0, 0, nullptr};
+    applySemantics(c0);
+    shaped.assign(works, works + nWorks);
+    for (auto& w : shaped) {
+      CallShape c{datatype, op, w.nSrcs, w.nPreOpSrcs, w.postOp, nullptr};
+      applySemantics(c);
+      w.nSrcs = c.nSrcs;
+      w.nPreOpSrcs = c.nPreOp;
+      w.postOp = c.postOp;
+    }
+    works = shaped.data();
+    datatype = c0.dt;
+    op = c0.op;
+  }
   const size_t esz = typeSize(datatype);
   for (int k = 1; k <= NEXR_MAX_SRCS; k++) {
     const uint64_t cap = gridCap(block_for(datatype, k));
@@ -240,14 +318,16 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, op, redOpArg, nPreOpSrcs, preOpArgs);
   if (r != nexrSuccess) return r;
   if (nElts == 0 || nDsts == 0) return nexrSuccess;  // common_kernel.h:288-289: nothing to store
-  const size_t esz = typeSize(datatype);
+  CallShape c{datatype, op, nSrcs, nPreOpSrcs, postOp, prePtr};
+  applySemantics(c);
+  const size_t esz = typeSize(c.dt);
   RCParams p;
-  fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, nPreOpSrcs, preOpArgs, prePtr, postOp);
+  fillParams(p, c.nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, c.nPreOp, preOpArgs, c.prePtr, c.postOp);
   Geometry g;
-  r = pickGeometry(workgroupsFor(p, nSrcs, datatype), (uint64_t)(nSrcs + nDsts) * nElts * esz,
-                   block_for(datatype, nSrcs), &g);
+  r = pickGeometry(workgroupsFor(p, c.nSrcs, c.dt), (uint64_t)(c.nSrcs + nDsts) * nElts * esz,
+                   block_for(c.dt, c.nSrcs), &g);
   if (r != nexrSuccess) return r;
-  NEXR_HIP(launchDt(datatype, p, op, nSrcs, g, stream));
+  NEXR_HIP(launchDt(c.dt, p, c.op, c.nSrcs, g, stream));
   return nexrSuccess;
 }
 
@@ -780,6 +860,9 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
   nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, nexrDevSum, 0, 0, nullptr);
   if (r != nexrSuccess) return r;
   if (nElts == 0 || nDsts == 0) return nexrSuccess;  // nothing would be launched
+  CallShape c{datatype, nexrDevSum, nSrcs, 0, 0, nullptr};
+  applySemantics(c);
+  nSrcs = c.nSrcs;
   const size_t esz = typeSize(datatype);
   RCParams p;
   fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, 0, 0, nullptr, nullptr, 0);
@@ -1032,6 +1115,7 @@ NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRec
   a.nSend = nSend;
   a.srcIsInput = srcIsInput ? 1 : 0;
   a.postOp = postOp ? 1 : 0;
+  llSemantics(&datatype, &devRedOp, &a.srcIsInput, &a.postOp, &a.firstWins);
   const uint64_t nPairs = (nElts * typeSize(datatype) + 15) / 16;
   uint64_t grid = (nPairs + kBlock - 1) / kBlock;
   if (grid > (1u << 20)) grid = 1u << 20;
@@ -1079,10 +1163,23 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
   a.nSend = nSend;
   a.srcIsInput = srcIsInput ? 1 : 0;
   a.postOp = postOp ? 1 : 0;
+  llSemantics(&datatype, &devRedOp, &a.srcIsInput, &a.postOp, &a.firstWins);
   const uint64_t nUnits = (nElts * typeSize(datatype) + kLL128SliceData - 1) / kLL128SliceData * 128;
   uint64_t grid = (nUnits + kBlock - 1) / kBlock;
   if (grid > (1u << 20)) grid = 1u << 20;
   NEXR_HIP(launch_ll128(datatype, a, devRedOp, (int)grid, (hipStream_t)stream));
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrSetSemantics(int mode) {
+  if (mode < 0 || mode >= nexrNumSemantics) return nexrInvalidArgument;
+  gSemantics.store(mode, std::memory_order_relaxed);
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrGetSemantics(int* mode) {
+  if (mode == nullptr) return nexrInvalidArgument;
+  *mode = semantics();
   return nexrSuccess;
 }
 

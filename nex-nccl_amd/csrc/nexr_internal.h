@@ -45,6 +45,7 @@ struct LLParams {
   uint32_t* status;                 // set to 1 when a recv flag never arrived (nullable)
   uint64_t timeoutTicks;            // s_memrealtime ticks (100 MHz) before giving up
   int nRecv, nSend, srcIsInput, postOp;
+  int firstWins;                    // nexrSemanticsShipped: every reduce returns its first operand
 };
 hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s);
 
@@ -64,6 +65,7 @@ struct LL128Params {
   uint32_t* status;
   uint64_t timeoutTicks;
   int nRecv, nSend, srcIsInput, postOp;
+  int firstWins;  // as LLParams
 };
 hipError_t launch_ll128(int dt, const LL128Params& a, int op, int grid, hipStream_t s);
 

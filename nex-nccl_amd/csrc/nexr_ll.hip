@@ -77,7 +77,7 @@ __device__ __forceinline__ void ll_pair(const LLParams& a, uint64_t pair) {
     if (i >= a.nRecv) break;
     u32x4 peer;
     if (!read_lines(a.recv[i] + pair * 32, nLines, a.recvFlag[i], a, &peer)) return;
-    if (i == 0 && !a.src) d = peer;
+    if ((i == 0 && !a.src) || a.firstWins) d = peer;  // SKIP_COMP: applyReduce returns the peer
     else d = bc<u32x4>(reduce_step<D, OP, IsMin>(bc<V>(peer), bc<V>(d)));  // applyReduce(redOp, peer, d)
   }
   if constexpr (OP == nexrDevSumPostDiv) {
@@ -85,7 +85,8 @@ __device__ __forceinline__ void ll_pair(const LLParams& a, uint64_t pair) {
   }
   if constexpr (D == nexrFloat16) {
     // ncclFromFloat canonicalises NaN whenever arithmetic ran on the pack
-    const bool arith = (a.nRecv >= 1 && a.src) || a.nRecv >= 2 || (OP == nexrDevPreMulSum && a.src && a.srcIsInput);
+    const bool arith = !a.firstWins && ((a.nRecv >= 1 && a.src) || a.nRecv >= 2 ||
+                                        (OP == nexrDevPreMulSum && a.src && a.srcIsInput));
     if (arith) d = bc<u32x4>(T::canon(bc<V>(d)));
   }
   for (int i = 0; i < NEXR_MAX_DSTS; i++) {
@@ -211,14 +212,15 @@ __device__ __forceinline__ void ll128_unit(const LL128Params& a, uint64_t unit) 
     if (!wait_flag64(a.recv[i] + flagOff, a.recvFlag[i], a.timeoutTicks, a.status)) return;
     const uint64_t lo = ld_sys(a.recv[i] + wireOff), hi = ld_sys(a.recv[i] + wireOff + 8);
     const u32x4 peer = (u32x4){(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-    if (i == 0 && !a.src) d = peer;
+    if ((i == 0 && !a.src) || a.firstWins) d = peer;
     else d = bc<u32x4>(reduce_step<D, OP, IsMin>(bc<V>(peer), bc<V>(d)));
   }
   if constexpr (OP == nexrDevSumPostDiv) {
     if (a.postOp) d = bc<u32x4>(T::divide(bc<V>(d), a.redArg));
   }
   if constexpr (D == nexrFloat16) {
-    const bool arith = (a.nRecv >= 1 && a.src) || a.nRecv >= 2 || (OP == nexrDevPreMulSum && a.src && a.srcIsInput);
+    const bool arith = !a.firstWins && ((a.nRecv >= 1 && a.src) || a.nRecv >= 2 ||
+                                        (OP == nexrDevPreMulSum && a.src && a.srcIsInput));
     if (arith) d = bc<u32x4>(T::canon(bc<V>(d)));
   }
   const uint64_t lo = ((uint64_t)d.y << 32) | d.x, hi = ((uint64_t)d.w << 32) | d.z;

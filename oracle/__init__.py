@@ -52,6 +52,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_float_to_bf16.restype = ctypes.c_uint16
         L.oracle_type_size.argtypes = [i32]
         L.oracle_type_size.restype = sz
+        L.oracle_set_semantics.argtypes = [i32]
+        L.oracle_set_semantics.restype = i32
+        L.oracle_get_semantics.argtypes = []
+        L.oracle_get_semantics.restype = i32
         _lib = L
     return _lib
 
@@ -96,6 +100,32 @@ def reduce_copy(srcs: Sequence[np.ndarray], n_dsts: int, datatype: int, dev_red_
     if rc != 0:
         raise ValueError(f"oracle rejected arguments (rc={rc})")
     return list(dsts)
+
+
+def set_semantics(mode: int) -> None:
+    """Reduction semantics of every later oracle call (0 nccl, 1 fork, 2 shipped: include/nexr.h)."""
+    if lib().oracle_set_semantics(int(mode)) != 0:
+        raise ValueError(f"bad semantics {mode}")
+
+
+def get_semantics() -> int:
+    return int(lib().oracle_get_semantics())
+
+
+class semantics:
+    """Context manager: run a block under one semantics, restoring the previous one after."""
+
+    def __init__(self, mode: int):
+        self.mode = int(mode)
+
+    def __enter__(self):
+        self.prev = get_semantics()
+        set_semantics(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_semantics(self.prev)
+        return False
 
 
 def host_to_dev_red_op(op: int, datatype: int, n_ranks: int):

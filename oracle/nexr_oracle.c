@@ -120,6 +120,29 @@ static inline void make_fn(Fn* fn, int op, uint64_t arg) {
   fn->isSigned = (arg & 1) != 0;
 }
 
+/* ---- reduction semantics (include/nexr.h nexrSemantics_t), process-wide like the library's ------
+ * 0 nccl:    real arithmetic, min/max at the user's signedness (the default);
+ * 1 fork:    real arithmetic under the fork's dispatch — signed min/max run on the unsigned kernel
+ *            (generate.py:128-136), whose FuncMinMax ignores the sign xormask (reduce_kernel.h:59-65);
+ * 2 shipped: SKIP_COMP (reduce_kernel.h:432) — ncclReduceScalar returns its first operand, the
+ *            PreMulSum pre-op and SumPostDiv post-op return their input (:434-539). */
+static int g_semantics = 0;
+int oracle_set_semantics(int s) {
+  if (s < 0 || s > 2) return 4;
+  g_semantics = s;
+  return 0;
+}
+int oracle_get_semantics(void) { return g_semantics; }
+static int fork_dispatch_type(int dt, int op) {
+  if (op != 2 /* OP_MINMAX */) return dt;
+  return dt == 0 ? 1 : dt == 2 ? 3 : dt == 4 ? 5 : dt; /* i8 -> u8, i32 -> u32, i64 -> u64 */
+}
+/* A SIMPLE reduceCopy call as the semantics run it: shipped = a K = 1 copy of srcs[0]. */
+static void semantics_shape(int* dt, int* op, int* nSrcs, int* nPreOp, int* postOp) {
+  if (g_semantics == 1) *dt = fork_dispatch_type(*dt, *op);
+  if (g_semantics == 2) { *op = 0; *nSrcs = 1; *nPreOp = 0; *postOp = 0; }
+}
+
 #define MINMAX(isMin, c, v) ((isMin) ? ((v) < (c) ? (v) : (c)) : ((v) > (c) ? (v) : (c)))
 
 /* unsigned-representation integer ops (sum/prod wrap), signed compare where the type is signed */
@@ -269,6 +292,7 @@ int oracle_reduce_copy(int nSrcs, const void* const* srcs, int nDsts, void* cons
                        const uint64_t* preOpArgs, int postOp) {
   int r = check(nSrcs, nDsts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
   if (r != R_OK) return r;
+  semantics_shape(&datatype, &devRedOp, &nSrcs, &nPreOpSrcs, &postOp);
   Job j = {nSrcs, nDsts, datatype, devRedOp, nPreOpSrcs, postOp, srcs, dsts, preOpArgs, redOpArg, 0, nElts};
   run_job(&j);
   return R_OK;
@@ -293,6 +317,7 @@ int oracle_reduce_copy_mt(int nSrcs, const void* const* srcs, int nDsts, void* c
                           const uint64_t* preOpArgs, int postOp, int nThreads) {
   int r = check(nSrcs, nDsts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs);
   if (r != R_OK) return r;
+  semantics_shape(&datatype, &devRedOp, &nSrcs, &nPreOpSrcs, &postOp);
   if (nThreads < 1) nThreads = 1;
   if (nThreads > 256) nThreads = 256;
   pthread_t th[256];
@@ -429,6 +454,7 @@ int oracle_reduce_copy_emulated(int nSrcs, const void* const* srcs, int nDsts, v
   if (r != R_OK) return r;
   if (nThreads < 32 || nThreads > 1024 || nThreads % 32 || unroll < 1 || unroll > 8) return R_INVALID;
   if (nDsts == 0 || nElts == 0) return R_OK; /* :288-289 */
+  semantics_shape(&datatype, &devRedOp, &nSrcs, &nPreOpSrcs, &postOp);
   EJob j = {nSrcs, nDsts, datatype, nPreOpSrcs, postOp, nThreads, unroll, (const char* const*)srcs,
             (char* const*)dsts, preOpArgs, {0, 0, 0, 0}};
   make_fn(&j.fn, devRedOp, redOpArg);
@@ -559,6 +585,9 @@ int oracle_reduce_copy_ll(const void* src, int srcIsInput, int nRecv, const void
   int r = check(1, 0, datatype, devRedOp, redOpArg, 0, NULL);
   if (r != R_OK) return r;
   if (nRecv < 0 || nRecv > 8 || nSend < 0 || nSend > 8 || (!src && !nRecv) || (!dst && !nSend)) return R_INVALID;
+  const int firstWins = g_semantics == 2; /* SKIP_COMP: applyReduce(redOp, peer, d) returns the peer */
+  if (g_semantics == 1) datatype = fork_dispatch_type(datatype, devRedOp);
+  if (firstWins) { srcIsInput = 0; postOp = 0; }
   Fn fn;
   make_fn(&fn, devRedOp, redOpArg);
   const size_t esz = oracle_type_size(datatype);
@@ -581,7 +610,7 @@ int oracle_reduce_copy_ll(const void* src, int srcIsInput, int nRecv, const void
       uint8_t peer[8];
       memcpy(peer, line, 4);
       memcpy(peer + 4, line + 8, 4);
-      if (i == 0 && !src) memcpy(d, peer, 8);
+      if ((i == 0 && !src) || firstWins) memcpy(d, peer, 8);
       else
         for (size_t e = 0; e < epl; e++) elem_reduce(datatype, &fn, peer + e * esz, d + e * esz, d + e * esz);
     }
@@ -624,6 +653,9 @@ int oracle_reduce_copy_ll128(const void* src, int srcIsInput, int nRecv, const v
   int r = check(1, 0, datatype, devRedOp, redOpArg, 0, NULL);
   if (r != R_OK) return r;
   if (nRecv < 0 || nRecv > 8 || nSend < 0 || nSend > 8 || (!src && !nRecv) || (!dst && !nSend)) return R_INVALID;
+  const int firstWins = g_semantics == 2; /* SKIP_COMP: every applyReduce returns the peer's words */
+  if (g_semantics == 1) datatype = fork_dispatch_type(datatype, devRedOp);
+  if (firstWins) { srcIsInput = 0; postOp = 0; }
   Fn fn;
   make_fn(&fn, devRedOp, redOpArg);
   const size_t esz = oracle_type_size(datatype);
@@ -663,7 +695,7 @@ int oracle_reduce_copy_ll128(const void* src, int srcIsInput, int nRecv, const v
       for (int i = 0; i < nRecv; i++) {
         for (int u = 0; u < 8; u += 2) {
           const uint8_t* wp = (const uint8_t*)recvWire[i] + 8 * (wBase + u * 32 + 2 * wid);
-          ll128_words(datatype, &fn, devRedOp, &v[u], 2, wp, (i == 0 && !src) ? 0 : 1);
+          ll128_words(datatype, &fn, devRedOp, &v[u], 2, wp, ((i == 0 && !src) || firstWins) ? 0 : 1);
         }
       }
       if (devRedOp == OP_SUMPOSTDIV && postOp)

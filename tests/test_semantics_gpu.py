@@ -1,0 +1,110 @@
+"""GPU parity of the HIP path in the two fork modes (include/nexr.h nexrSemantics_t): the library and
+the oracle are switched together, and the existing parity suites — whose expected values all come from
+the oracle — are rerun unchanged under each mode:
+
+  fork     the fork with SKIP_COMP removed (signed min/max compare as unsigned, generate.py:128-136)
+  shipped  the fork as shipped (SKIP_COMP, reduce_kernel.h:432: every reduce keeps its first operand)
+
+plus direct checks of the shipped build: the BASELINE C2 call at full size returns src0's bits, and the
+known answer SURVEY §0 records from the shipped tree (a[7] = 3.5 where the sum is 4.75).
+"""
+import numpy as np
+import pytest
+
+import make_golden as mg
+import test_batch_gpu as batch_t
+import test_ll128_gpu as ll128_t
+import test_ll_gpu as ll_t
+import test_reduce_copy_gpu as rc_t
+import test_ring_gpu as ring_t
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+FORK, SHIPPED = 1, 2
+
+
+@pytest.fixture(params=[FORK, SHIPPED], ids=["fork", "shipped"])
+def mode(request, nexr, oracle):
+    nexr.set_semantics(request.param)
+    oracle.set_semantics(request.param)
+    try:
+        yield request.param
+    finally:
+        nexr.set_semantics(0)
+        oracle.set_semantics(0)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("dt", sorted(mg.DT_NAMES))
+def test_all_ops_k_m(nexr, oracle, dt, dev, mode):
+    rc_t.test_matches_oracle_all_ops_k_m(nexr, oracle, dt, dev)
+
+
+@pytest.mark.parametrize("dt", [mg.I8, mg.F16, mg.F32, mg.BF16, mg.U64])
+def test_unaligned(nexr, oracle, dt, dev, mode):
+    rc_t.test_unaligned_heads_tails_and_phases(nexr, oracle, dt, dev)
+
+
+def test_fuzz(nexr, oracle, dev, mode):
+    rc_t.test_random_fuzz_against_oracle(nexr, oracle, dev)
+
+
+def test_in_place_host_staged_and_one_rank(nexr, oracle, dev, mode):
+    rc_t.test_in_place_dst_aliases_src0(nexr, oracle, dev)
+    rc_t.test_host_staged_variant(nexr, oracle, dev)
+    rc_t.test_one_rank_launcher(nexr, oracle, dev)
+
+
+@pytest.mark.parametrize("dt", [mg.I8, mg.I32, mg.F16, mg.BF16, mg.F64])
+def test_batch(nexr, oracle, dt, dev, mode):
+    batch_t.test_batch_mixed_works_match_oracle(nexr, oracle, dt, dev)
+    if dt == mg.I8:
+        batch_t.test_batch_min_and_max_in_one_launch(nexr, oracle, dev)
+
+
+@pytest.mark.parametrize("dt", [mg.I8, mg.I32, mg.I64, mg.F16, mg.BF16, mg.F32])
+def test_ll_and_ll128_steps(nexr, oracle, dt, mode):
+    ll_t.test_ll_all_ops_and_shapes(nexr, oracle, dt)
+    ll128_t.test_ll128_all_ops_and_shapes(nexr, oracle, dt)
+
+
+@pytest.mark.parametrize("n_ranks,dt,op", [(2, mg.F32, 0), (3, mg.I32, 3), (4, mg.I8, 2), (3, mg.F16, 4)])
+def test_ring_collectives(nexr, oracle, n_ranks, dt, op, mode):
+    import importlib
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    ring_t.test_ring_device_memory_matches_fold_order(ring, oracle, n_ranks, dt, op)
+    ring_t.test_ll_ring_device_memory(ring, oracle, n_ranks, dt, op)
+
+
+def test_shipped_known_answer_and_full_size_c2(nexr, oracle, dev):
+    """the shipped tree's fp32 sum returns src0 (a[7] = 3.5); the BASELINE C2 call at full
+    size (2 x 256 MiB -> 256 MiB) returns src0's bits, NaN payloads and all, in the shipped build."""
+    try:
+        nexr.set_semantics(SHIPPED)
+        a = torch.tensor([0.5 * i for i in range(16)], dtype=torch.float32, device="cuda")
+        b = torch.full((16,), 1.25, dtype=torch.float32, device="cuda")
+        o = torch.empty_like(a)
+        nexr.reduce_copy([a, b], [o], mg.SUM)
+        torch.cuda.synchronize()
+        assert o[7].item() == 3.5 and torch.equal(o.view(torch.int32), a.view(torch.int32))
+        n = 64 << 20
+        g = torch.Generator(device="cuda")
+        g.manual_seed(3)
+        a = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        b = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        o = torch.empty_like(a)
+        nexr.reduce_copy([a.view(torch.float32), b.view(torch.float32)], [o.view(torch.float32)], mg.SUM)
+        torch.cuda.synchronize()
+        assert torch.equal(o, a)
+        nexr.set_semantics(0)
+        nexr.reduce_copy([a.view(torch.float32), b.view(torch.float32)], [o.view(torch.float32)], mg.SUM)
+        torch.cuda.synchronize()
+        assert not torch.equal(o, a)
+    finally:
+        nexr.set_semantics(0)
