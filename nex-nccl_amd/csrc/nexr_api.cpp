@@ -109,26 +109,31 @@ void llSemantics(int* dt, int* op, int* srcIsInput, int* postOp, int* firstWins)
   }
 }
 
-// Grid: one workgroup per kTripPacks-pack trip ("one-shot"), capped so that grid x block stays
-// within HIP's 2^32 - 1 work-item limit (2^24 workgroups of 256 lanes, 2^22 of 1024); beyond the
-// cap the kernel grid-strides. Policy by the bytes the call streams (every src read once, every
-// dst written once): plain below NEXR_NT_LOAD_MIN_BYTES (64 MiB: the data likely sits in L2/MALL
-// and the consumer wants the output there too), non-temporal loads above it, non-temporal loads
-// and stores above NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3)
-// and NEXR_GRID override for sweeps.
-uint64_t gridCap(int block) { return 0xffffffffull / (uint64_t)block; }
-
-nexrResult_t pickGeometry(uint64_t workgroups, uint64_t streamBytes, int block, Geometry* g) {
-  static const long gridOverride = envLong("NEXR_GRID", 0);
+// Cache policy by the bytes a call streams (every src read once, every dst written once): plain below
+// NEXR_NT_LOAD_MIN_BYTES (64 MiB: the data likely sits in L2/MALL and the consumer wants the output
+// there too), non-temporal loads above it, non-temporal loads and stores above
+// NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3) overrides it for
+// sweeps. The workgroup geometry follows the policy (unroll_for/block_for, nexr_internal.h).
+int pickPolicy(uint64_t streamBytes) {
   static const long polOverride = envLong("NEXR_POLICY", -1);
   static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);
   static const long ntStoreMin = envLong("NEXR_NT_STORE_MIN_BYTES", 512l << 20);
+  if (polOverride >= 0) return polOverride == 0 ? 0 : (polOverride == 1 ? 1 : 3);
+  return streamBytes >= (uint64_t)ntStoreMin ? 3 : (streamBytes >= (uint64_t)ntLoadMin ? 1 : 0);
+}
+
+// Grid: one workgroup per kTripPacks-pack trip ("one-shot"), capped so that grid x block stays
+// within HIP's 2^32 - 1 work-item limit (2^24 workgroups of 256 lanes, 2^22 of 1024); beyond the
+// cap the kernel grid-strides. NEXR_GRID overrides the grid for sweeps.
+uint64_t gridCap(int block) { return 0xffffffffull / (uint64_t)block; }
+
+nexrResult_t pickGeometry(uint64_t workgroups, int pol, int block, Geometry* g) {
+  static const long gridOverride = envLong("NEXR_GRID", 0);
   const uint64_t cap = gridCap(block);
   uint64_t need = workgroups < 1 ? 1 : workgroups;
   g->grid = (int)(need < cap ? need : cap);
   if (gridOverride > 0) g->grid = (int)gridOverride;
-  if (polOverride >= 0) g->pol = polOverride == 0 ? 0 : (polOverride == 1 ? 1 : 3);
-  else g->pol = streamBytes >= (uint64_t)ntStoreMin ? 3 : (streamBytes >= (uint64_t)ntLoadMin ? 1 : 0);
+  g->pol = pol;
   return nexrSuccess;
 }
 
@@ -214,8 +219,8 @@ void fillParams(RCParams& p, int nSrcs, const void* const* srcs, int nDsts, void
 
 // One-shot workgroups of one reduce-copy: one per B lane work items, a work item being an element
 // (generic path) or a U-pack group (packed path), with (U, B) = the kernel's geometry for (dt, K).
-uint64_t workgroupsFor(const RCParams& p, int nSrcs, int dt) {
-  const uint64_t u = (uint64_t)unroll_for(dt, nSrcs), b = (uint64_t)block_for(dt, nSrcs);
+uint64_t workgroupsFor(const RCParams& p, int nSrcs, int dt, int pol) {
+  const uint64_t u = (uint64_t)unroll_for(dt, nSrcs, pol), b = (uint64_t)block_for(dt, nSrcs, pol);
   const uint64_t items = p.generic ? p.nElts : (p.nPacks + u - 1) / u;
   return (items + b - 1) / b;
 }
@@ -265,16 +270,25 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
   }
   const size_t esz = typeSize(datatype);
   for (int k = 1; k <= NEXR_MAX_SRCS; k++) {
-    const uint64_t cap = gridCap(block_for(datatype, k));
     BatchParams b;
     b.nWorks = 0;
     uint64_t blocks[kMaxBatch];
     uint64_t streamBytes = 0;
+    // One launch per run of works: the policy (and with it the geometry) from the bytes the whole
+    // launch streams, then work i gets its one-shot grid, the total capped at gridCap(block) by
+    // halving the largest shares (rare: > 4 G packed items; the kernel grid-strides inside a work).
     auto flush = [&]() -> nexrResult_t {
       if (b.nWorks == 0) return nexrSuccess;
+      const int pol = pickPolicy(streamBytes);
+      const int block = block_for(datatype, k, pol);
+      const uint64_t cap = gridCap(block);
       uint64_t total = 0;
-      for (int i = 0; i < b.nWorks; i++) total += blocks[i];
-      while (total > cap) {  // rare (> 4 G packed items): halve the largest share
+      for (int i = 0; i < b.nWorks; i++) {
+        const uint64_t need = workgroupsFor(b.w[i], k, datatype, pol);
+        blocks[i] = need < 1 ? 1 : (need < cap ? need : cap);
+        total += blocks[i];
+      }
+      while (total > cap) {
         int big = 0;
         for (int i = 1; i < b.nWorks; i++)
           if (blocks[i] > blocks[big]) big = i;
@@ -285,7 +299,7 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
       b.start[0] = 0;
       for (int i = 0; i < b.nWorks; i++) b.start[i + 1] = b.start[i] + (uint32_t)blocks[i];
       Geometry g;
-      nexrResult_t r = pickGeometry(total, streamBytes, block_for(datatype, k), &g);
+      nexrResult_t r = pickGeometry(total, pol, block, &g);
       if (r != nexrSuccess) return r;
       NEXR_HIP(launchBatchDt(datatype, b, op, k, g.pol, (int)total, stream));
       b.nWorks = 0;
@@ -298,8 +312,6 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
       RCParams& p = b.w[b.nWorks];
       fillParams(p, k, w.srcs, w.nDsts, w.dsts, w.nElts, esz, w.redOpArg, w.nPreOpSrcs, w.preOpArgs, nullptr,
                  w.postOp);
-      uint64_t need = workgroupsFor(p, k, datatype);
-      blocks[b.nWorks] = need < 1 ? 1 : (need < cap ? need : cap);
       streamBytes += (uint64_t)(k + w.nDsts) * w.nElts * esz;
       if (++b.nWorks == kMaxBatch) {
         nexrResult_t r = flush();
@@ -324,8 +336,8 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   RCParams p;
   fillParams(p, c.nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, c.nPreOp, preOpArgs, c.prePtr, c.postOp);
   Geometry g;
-  r = pickGeometry(workgroupsFor(p, c.nSrcs, c.dt), (uint64_t)(c.nSrcs + nDsts) * nElts * esz,
-                   block_for(c.dt, c.nSrcs), &g);
+  const int pol = pickPolicy((uint64_t)(c.nSrcs + nDsts) * nElts * esz);
+  r = pickGeometry(workgroupsFor(p, c.nSrcs, c.dt, pol), pol, block_for(c.dt, c.nSrcs, pol), &g);
   if (r != nexrSuccess) return r;
   NEXR_HIP(launchDt(c.dt, p, c.op, c.nSrcs, g, stream));
   return nexrSuccess;
@@ -867,12 +879,13 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
   RCParams p;
   fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, 0, 0, nullptr, nullptr, 0);
   Geometry g;
-  const int block = block_for(datatype, nSrcs);
-  r = pickGeometry(workgroupsFor(p, nSrcs, datatype), (uint64_t)(nSrcs + nDsts) * nElts * esz, block, &g);
+  const int pol = pickPolicy((uint64_t)(nSrcs + nDsts) * nElts * esz);
+  const int block = block_for(datatype, nSrcs, pol);
+  r = pickGeometry(workgroupsFor(p, nSrcs, datatype, pol), pol, block, &g);
   if (r != nexrSuccess) return r;
   info->grid = (uint32_t)g.grid;
   info->block = block;
-  info->packsPerLane = p.generic ? 1 : unroll_for(datatype, nSrcs);
+  info->packsPerLane = p.generic ? 1 : unroll_for(datatype, nSrcs, pol);
   info->policy = g.pol;
   info->generic = p.generic;
   info->headElts = p.head;

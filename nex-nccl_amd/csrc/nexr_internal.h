@@ -100,17 +100,27 @@ NEXR_DECLARE_BATCH(4) NEXR_DECLARE_BATCH(5) NEXR_DECLARE_BATCH(6) NEXR_DECLARE_B
 NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 #undef NEXR_DECLARE_BATCH
 
-// Workgroup geometry per (datatype, fan-in): U packs per lane x B lanes per workgroup, always one
-// trip of kTripPacks 16-B packs (16 KiB) per buffer, so the grid is nPacks / kTripPacks either way.
-// Steady-state sweeps over U in {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8
-// (tools/tune_kernel.hip, tools/tune_sched.hip TUNE_MODE=geom; profiles/r01_tune_*.log,
-// r01_skew.log, r01s2_geom_*.log): U = 4, B = 256 is best or within noise of best everywhere except
-// the 16-bit floats with K = 8, where U = 1, B = 1024 (16 waves) is faster: fp16 399.9 vs 407.9 us,
-// bf16 394.9 vs 402.0 us in same-box A/Bs alternated six times (profiles/r01s3_*_geometry_ab.txt).
+// Workgroup geometry per (datatype, fan-in, cache policy): U packs per lane x B lanes per workgroup,
+// always one trip of kTripPacks 16-B packs (16 KiB) per buffer, so the grid is nPacks / kTripPacks
+// whatever the geometry. U = 4, B = 256 is the default (round-1 steady-state sweeps over U in
+// {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8: profiles/r01_tune_*.log,
+// r01_skew.log, r01s2_geom_*.log). Three exceptions, each measured in one process against the default
+// on several boxes with byte-identical outputs:
+//   - 16-bit floats, K >= 8 (any size): U = 1, B = 1024 — fp16 399.9 vs 407.9 us, bf16 394.9 vs
+//     402.0 us at C3 in same-box A/Bs alternated six times (profiles/r01s3_*_geometry_ab.txt);
+//   - K = 4 with non-temporal loads and cached stores (64-512 MiB streamed, C4's regime): U = 2,
+//     B = 512 — +0.9 % on average over 9 datatypes x {sum, min} on four boxes, never below -0.7 %
+//     (tools/geom_sweep.hip, profiles/r02_geom_sweep_*.log; int8 min/max/prod +1-2 %);
+//   - K = 4 with non-temporal loads and stores (>= 512 MiB streamed), every type but fp16: U = 1,
+//     B = 1024 — +0.5-4 % (+2 % on average) on the same boxes; fp16 alone is mixed there.
+// K = 2 keeps the default everywhere (U = 1 loses 10-13 %, U = 2 loses 1-5 %).
 constexpr int kTripPacks = 1024;
-__host__ __device__ constexpr int unroll_for(int dt, int k) {
-  return (dt == nexrFloat16 || dt == nexrBfloat16) && k >= 8 ? 1 : 4;
+__host__ __device__ constexpr int unroll_for(int dt, int k, int pol) {
+  return ((dt == nexrFloat16 || dt == nexrBfloat16) && k >= 8) ? 1
+         : (k == 4 && pol == 1)                                 ? 2
+         : (k == 4 && pol == 3 && dt != nexrFloat16)            ? 1
+                                                                : 4;
 }
-__host__ __device__ constexpr int block_for(int dt, int k) { return kTripPacks / unroll_for(dt, k); }
+__host__ __device__ constexpr int block_for(int dt, int k, int pol) { return kTripPacks / unroll_for(dt, k, pol); }
 
 }  // namespace nexr

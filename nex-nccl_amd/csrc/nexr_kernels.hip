@@ -4,11 +4,11 @@
 // What it computes is the reference's reduceCopy (src/device/common_kernel.h:269-349 →
 // reduceCopyPacks :141-253) with the real per-type arithmetic of src/device/reduce_kernel.h
 // (:238-539, SKIP_COMP at :432 removed). How it computes it is MI355X-first:
-//   - one 16-B load per lane per source per pack (global_load_dwordx4), 64-lane waves,
-//     4 waves per workgroup; each workgroup owns one 16 KiB trip of every buffer (U = 4 packs
-//     per lane, "one-shot" grid of nPacks/(256*4) workgroups; a grid-stride loop only beyond
-//     (2^32-1)/block workgroups, HIP's work-item limit), so every lane has 4*K independent loads
-//     in flight;
+//   - one 16-B load per lane per source per pack (global_load_dwordx4), 64-lane waves; each
+//     workgroup owns one 16 KiB trip of every buffer (U packs per lane x B lanes = 1024 packs,
+//     by default U = 4 with 4 waves; unroll_for/block_for in nexr_internal.h), a "one-shot" grid of
+//     nPacks/1024 workgroups (a grid-stride loop only beyond (2^32-1)/B workgroups, HIP's
+//     work-item limit), so every lane has U*K independent loads in flight;
 //   - all K source loads of a trip are issued before the first reduce step;
 //   - cache policy by working-set size: non-temporal loads once a call streams more than
 //     64 MiB, non-temporal loads AND stores beyond 512 MiB (2x the Infinity Cache) —
@@ -185,7 +185,7 @@ __device__ __forceinline__ void dispatch_minmax(const RCParams& p, uint64_t bid,
   }
 }
 
-template <int D, int OP, int K, int POL, int U = unroll_for(D, K), int B = block_for(D, K)>
+template <int D, int OP, int K, int POL, int U = unroll_for(D, K, POL), int B = block_for(D, K, POL)>
 __global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
   dispatch_minmax<D, OP, K, POL, U, B>(p, blockIdx.x, gridDim.x);
 }
@@ -195,11 +195,11 @@ __global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
 // owns workgroups [start[i], start[i+1]). The work index is wave-uniform, so the descriptor is read
 // straight from the kernel-argument segment with scalar loads.
 template <int D, int OP, int K, int POL>
-__global__ __launch_bounds__(block_for(D, K)) void reduce_copy_batch_kernel(BatchParams b) {
+__global__ __launch_bounds__(block_for(D, K, POL)) void reduce_copy_batch_kernel(BatchParams b) {
   int i = 0;
   while (i + 1 < b.nWorks && blockIdx.x >= b.start[i + 1]) i++;
-  dispatch_minmax<D, OP, K, POL, unroll_for(D, K), block_for(D, K)>(b.w[i], blockIdx.x - b.start[i],
-                                                                      b.start[i + 1] - b.start[i]);
+  dispatch_minmax<D, OP, K, POL, unroll_for(D, K, POL), block_for(D, K, POL)>(b.w[i], blockIdx.x - b.start[i],
+                                                                                b.start[i + 1] - b.start[i]);
 }
 
 template <int D, int OP, int K>
@@ -208,7 +208,7 @@ static hipError_t launch_k(const RCParams& p, const Geometry& g, hipStream_t s) 
                    : g.pol == kPolNtLoad ? (const void*)&reduce_copy_kernel<D, OP, K, kPolNtLoad>
                                          : (const void*)&reduce_copy_kernel<D, OP, K, kPolPlain>;
   void* args[] = {const_cast<RCParams*>(&p)};
-  return hipLaunchKernel(fn, dim3(g.grid), dim3(block_for(D, K)), args, 0, s);
+  return hipLaunchKernel(fn, dim3(g.grid), dim3(block_for(D, K, g.pol)), args, 0, s);
 }
 
 template <int D, int OP>
@@ -232,7 +232,7 @@ static hipError_t launch_batch_k(const BatchParams& b, int pol, int grid, hipStr
                    : pol == kPolNtLoad ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNtLoad>
                                        : (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolPlain>;
   void* args[] = {const_cast<BatchParams*>(&b)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(block_for(D, K)), args, 0, s);
+  return hipLaunchKernel(fn, dim3(grid), dim3(block_for(D, K, pol)), args, 0, s);
 }
 
 template <int D, int OP>

@@ -1,7 +1,9 @@
-"""GPU tests of the per-(datatype, fan-in) workgroup geometry (nexr_internal.h unroll_for/block_for):
-fp16 with K = 8 runs 1024-lane workgroups with one pack per lane, every other shape 256 lanes with
-four. Sizes straddle the 16 KiB trip (the one-shot body, the per-pack remainder loop and the scalar
-edges), for the single launch and the batch launch, against the oracle bit for bit."""
+"""GPU tests of the per-(datatype, fan-in, cache policy) workgroup geometry (nexr_internal.h
+unroll_for/block_for): fp16/bf16 with K = 8 run 1024-lane workgroups with one pack per lane; K = 4
+runs 2 packs x 512 lanes once a call streams 64-512 MiB and 1 x 1024 beyond (fp16 excepted); every
+other shape 256 lanes with four. Sizes straddle the 16 KiB trip (the one-shot body, the per-pack
+remainder loop and the scalar edges), for the single launch and the batch launch, against the oracle
+bit for bit."""
 import numpy as np
 import pytest
 
@@ -68,3 +70,56 @@ def test_f16_k8_in_a_batch_beside_other_shapes(nexr, oracle, dev):
     torch.cuda.synchronize()
     for o, e in zip(outs, expect):
         assert mg.canon_bytes(mg.F16, o.cpu().numpy()) == mg.canon_bytes(mg.F16, e)
+
+
+# ---- K = 4: the geometry follows the cache policy -------------------------------------------------------
+MIB = 1 << 20
+
+
+@pytest.mark.parametrize("dt,op,name,buf_mib", [
+    (mg.I8, mg.MINMAX, "min", 16), (mg.I32, mg.PROD, "prod", 16), (mg.F32, mg.SUM, "sum", 13),  # 2 x 512
+    (mg.U32, mg.MINMAX, "max", 104), (mg.BF16, mg.SUM, "sum", 104),                              # 1 x 1024
+    (mg.F16, mg.SUM, "sum", 104)])                                                               # 4 x 256
+def test_k4_policy_geometries_edges(nexr, oracle, dev, dt, op, name, buf_mib):
+    esz = np.dtype(mg.STORE[dt]).itemsize
+    base = buf_mib * MIB // esz
+    arg = mg.minmax_arg(dt, name == "max") if op == mg.MINMAX else 0
+    for n, offs in ((base, None), (base + 16 // esz * 1024 * 3 + 5, None), (base - 7, [esz] * 5),
+                    (base + 1, [0, esz, 0, 2 * esz, esz])):
+        srcs = mg.gen_inputs(dt, 4, n, 4400 + n % 1013, special=True)
+        info = nexr.query_launch([0x100000 * (i + 1) + (offs[i] if offs else 0) for i in range(4)],
+                                 [0x900000 + (offs[4] if offs else 0)], n, dt)
+        if offs is None or len(set(offs)) == 1:
+            assert info.generic == 0 and info.block == (512 if info.policy == 1 else 256 if dt == mg.F16 else 1024)
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
+        got = _run(nexr, srcs, dt, op, arg, offs)
+        assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)
+        del srcs, exp, got
+        torch.cuda.empty_cache()
+
+
+def test_k4_batch_at_the_c4_policy(nexr, oracle, dev):
+    """A batch of K = 4 works streaming more than 64 MiB in total launches the 2 x 512 geometry;
+    each work's bytes must match the oracle, as must K = 2 works batched beside them (4 x 256)."""
+    rng = np.random.default_rng(44)
+    works, expect, outs, keep = [], [], [], []
+    for i in range(6):
+        k = 4 if i % 3 else 2
+        n = int(rng.integers(2 * MIB, 4 * MIB))
+        srcs = mg.gen_inputs(mg.I8, k, n, 700 + i, special=True)
+        ts = [torch.from_numpy(s.copy()).cuda() for s in srcs]
+        o = torch.zeros(n, dtype=ts[0].dtype, device="cuda")
+        keep += ts
+        outs.append(o)
+        arg = mg.minmax_arg(mg.I8, False)
+        works.append(nexr.make_work([t.data_ptr() for t in ts], [o.data_ptr()], n, arg))
+        expect.append(oracle.reduce_copy(srcs, 1, mg.I8, mg.MINMAX, arg)[0])
+    big = [torch.from_numpy(s.copy()).cuda() for s in mg.gen_inputs(mg.I8, 4, 16 * MIB, 799, special=True)]
+    ob = torch.zeros(16 * MIB, dtype=big[0].dtype, device="cuda")
+    works.append(nexr.make_work([t.data_ptr() for t in big], [ob.data_ptr()], 16 * MIB, mg.minmax_arg(mg.I8, False)))
+    expect.append(oracle.reduce_copy([t.cpu().numpy() for t in big], 1, mg.I8, mg.MINMAX, mg.minmax_arg(mg.I8, False))[0])
+    outs.append(ob)
+    nexr.reduce_copy_batch(works, mg.I8, mg.MINMAX, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for o, e in zip(outs, expect):
+        assert mg.canon_bytes(mg.I8, o.cpu().numpy()) == mg.canon_bytes(mg.I8, e)

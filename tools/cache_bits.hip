@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
   const int iters = argc > 2 ? atoi(argv[2]) : 8;
   constexpr int D = NEXR_DT, K = TK_K;
   constexpr int esz = 16 / Ty<D>::EPP;
-  constexpr int U = unroll_for(D, K), B = block_for(D, K);
+  constexpr int U = unroll_for(D, K, kPolNt), B = block_for(D, K, kPolNt);
   const int R = 3;  // rotating buffer sets, as the bench
   std::vector<RCParams> ps(R);
   for (int r = 0; r < R; r++) {

@@ -196,7 +196,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&nCU, hipDeviceAttributeMultiprocessorCount, 0));
   const double alg = (double)(K + 1) * bytes;
   const uint64_t P = bytes / 16;
-  constexpr int PU = unroll_for(D, K), PB = block_for(D, K);
+  constexpr int PU = unroll_for(D, K, kPolNt), PB = block_for(D, K, kPolNt);
   std::vector<Var> vs;
   vs.push_back({"production U" + std::to_string(PU) + " B" + std::to_string(PB),
                 [&](int r) { reduce_copy_kernel<D, 0, K, kPolNt, PU, PB><<<(int)(P / (PU * PB)), PB>>>(ps[r]); }, {}});
