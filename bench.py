@@ -465,19 +465,39 @@ def base_line(cfg, n_gpus: int, steps: int, warmup: int, value: float, max_s: fl
     }
 
 
-def xgmi_probe(timeout_s: float = 120.0):
-    """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, in a bounded
-    subprocess: its outcome is reported, never allowed to fail the bench line."""
+def _bounded(cmd, timeout_s: float):
+    """Run a probe in its own process group; on a timeout the whole group (the probe and the ring
+    ranks it started) is killed. Returns its last JSON line or an error record, never raises."""
+    import signal
     import subprocess
     try:
-        p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "xgmi_probe.py")], capture_output=True,
-                           text=True, timeout=timeout_s)
-        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+        try:
+            out, err = p.communicate(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.communicate()
+            return {"error": f"timeout after {timeout_s:.0f} s"}
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
         if p.returncode == 0 and lines:
             return json.loads(lines[-1])
-        return {"error": f"exit {p.returncode}", "stderr": p.stderr[-300:]}
+        return {"error": f"exit {p.returncode}", "stderr": err[-300:]}
     except Exception as e:  # noqa: BLE001 - reported, not raised
         return {"error": repr(e)[:300]}
+
+
+def xgmi_probe(timeout_s: float = 120.0):
+    """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, in bounded
+    subprocesses: GPU 0's kernel with an operand in GPU 1's HBM and the two-rank process ring; with
+    three or more GPUs also the process ring over all of them (up to 8). Reported, never allowed to
+    fail the bench line."""
+    import torch
+    probe = os.path.join(ROOT, "tools", "xgmi_probe.py")
+    res = _bounded([sys.executable, probe], timeout_s)
+    n_dev = torch.cuda.device_count()
+    if n_dev >= 3 and isinstance(res, dict) and "skipped" not in res:
+        res["ring_processes_all_gpus"] = _bounded([sys.executable, probe, "--ring-all", str(min(n_dev, 8))], 100.0)
+    return res
 
 
 def h2d_inclusive(pkg, cfg, reps: int = 3):

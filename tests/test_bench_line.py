@@ -151,3 +151,32 @@ def test_cpu_baseline_runs_the_full_configuration(monkeypatch):
     assert seen["first"] == (1, (480, 4))
     assert seen["modes"] == {(False, (480, 4)), (True, (480, 4)), (False, None), (True, None)}
     assert e["element_loop"]["cores"] == 1 and e["element_loop"]["all_cores"] == bench.usable_cores()[0]
+
+
+def test_bounded_probe_kills_its_whole_process_group(tmp_path):
+    """bench._bounded (the xGMI probes after the timed region): a probe that hangs is killed together
+    with the ring ranks it started, and the line records the timeout instead of failing."""
+    import subprocess
+    import sys
+    import time
+    pidfile = tmp_path / "grandchild.pid"
+    script = tmp_path / "hang.py"
+    script.write_text(
+        "import subprocess, sys, time\n"
+        f"g = subprocess.Popen([sys.executable, '-c', 'import time; time.sleep(600)'])\n"
+        f"open({str(pidfile)!r}, 'w').write(str(g.pid))\n"
+        "time.sleep(600)\n")
+    t0 = time.time()
+    res = bench._bounded([sys.executable, str(script)], 3.0)
+    assert "timeout" in res["error"] and time.time() - t0 < 30
+    gpid = int(pidfile.read_text())
+    for _ in range(50):
+        if subprocess.run(["kill", "-0", str(gpid)], capture_output=True).returncode != 0:
+            break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("the probe's child survived the timeout")
+    ok = bench._bounded([sys.executable, "-c", "print('{\"a\": 1}')"], 30.0)
+    assert ok == {"a": 1}
+    bad = bench._bounded([sys.executable, "-c", "import sys; sys.exit(3)"], 30.0)
+    assert bad["error"] == "exit 3"

@@ -10,9 +10,10 @@ enabled both ways, and the reduce-copy kernel run on GPU 0 with one operand in G
 fp32 sum, 256 MiB per buffer. Then the process-rank ring itself across the two GPUs
 (`ring_processes`): two child processes, rank r on GPU r, each mapping the other's FIFO over IPC
 (nexrPeerRingCommCreate), run the emulated ring all-reduce (C1's 4 MiB and 64 MiB of fp32 per rank,
-SIMPLE) with every step's reduce-copy writing into the peer GPU's HBM over xGMI; results are checked
-exactly (integer-valued inputs). Prints one JSON line; with fewer than two GPUs it prints a
-"skipped" line and exits 0. bench.py runs it as a bounded subprocess when it drives more than one
+SIMPLE; LL and LL128 at 4 MiB) with every step's reduce-copy writing into the peer GPU's HBM over
+xGMI; every rank's result is checked exactly (integer-valued inputs). `--ring-all N` runs the same
+ring with N processes on the first N GPUs. Prints one JSON line; with fewer than two GPUs it prints a
+"skipped" line and exits 0. bench.py runs it as bounded subprocesses when it drives more than one
 GPU, so a failure here can never take the bench line down with it.
 """
 import ctypes
@@ -93,22 +94,25 @@ PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2}
 LL_COUNT = 1 << 20  # the LL protocols run C1's 4 MiB only (they move 2x / 16/15x the payload)
 
 
-def ring_rank(rank: int, shm: str, counts) -> int:
+def ring_rank(rank: int, n_ranks: int, shm: str, counts) -> int:
     """One rank of the cross-GPU process ring (child process, GPU `rank`): the SIMPLE ring at every
-    count, then the LL and LL128 rings at C1's size, one communicator per protocol."""
+    count, then the LL and LL128 rings at C1's size, one communicator per protocol. Every rank checks
+    its own output exactly and prints its line."""
     import time
     import torch
-    dev = rank % torch.cuda.device_count()  # GPU r; both on GPU 0 when rehearsing on a one-GPU box
+    dev = rank % torch.cuda.device_count()  # GPU r; folded onto the visible GPUs when rehearsing
     torch.cuda.set_device(dev)
     ring = importlib.import_module("nex-nccl_amd.ring")
     out = {}
     for pname, proto in PROTOCOLS.items():
         out[pname] = res = {}
-        with ring.PeerRingComm(2, rank, f"{shm}_{pname}", device=dev, protocol=proto, timeout_ms=30000) as comm:
+        with ring.PeerRingComm(n_ranks, rank, f"{shm}_{pname}", device=dev, protocol=proto,
+                               timeout_ms=30000) as comm:
             for count in (counts if pname == "simple" else [LL_COUNT]):
                 x = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) + rank
                 y = torch.empty_like(x)
-                exp = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) * 2 + 1
+                exp = (torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) * n_ranks
+                       + n_ranks * (n_ranks - 1) // 2)
                 torch.cuda.synchronize()
                 comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)  # warm-up, connects the FIFOs
                 iters = 5
@@ -118,19 +122,21 @@ def ring_rank(rank: int, shm: str, counts) -> int:
                 dt = (time.perf_counter() - t0) / iters
                 res[str(count * 4)] = {"ms": round(dt * 1e3, 3), "algbw_GBps": round(count * 4 / dt / 1e9, 2),
                                        "exact": bool(torch.equal(y, exp))}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    print(json.dumps({"rank": rank, "gpu": dev, "results": out}), flush=True)
     return 0
 
 
-def ring_processes(timeout_s: float = 60.0):
+def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "1048576,16777216"):
+    """n_ranks child processes, rank r on GPU r mod visible, each mapping its successor's FIFO over IPC:
+    the ring all-reduce at C1's 4 MiB (SIMPLE, LL, LL128) and 64 MiB (SIMPLE). Reports rank 0's timing
+    and whether EVERY rank's output was exact. Children stay in this process's group, so a caller
+    that kills the group on a timeout ends them too; on this function's own timeout they are killed."""
     import subprocess
     import uuid
     shm = f"/nexr_xgmi_{uuid.uuid4().hex[:12]}"
-    counts = "1048576,16777216"
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--ring-rank", str(r), "--shm", shm,
-                               "--counts", counts], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                              start_new_session=True) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--ring-rank", str(r), "--ranks",
+                               str(n_ranks), "--shm", shm, "--counts", counts], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(n_ranks)]
     outs = []
     try:
         for p in procs:
@@ -138,26 +144,34 @@ def ring_processes(timeout_s: float = 60.0):
     except subprocess.TimeoutExpired:
         for p in procs:
             if p.poll() is None:
-                os.killpg(p.pid, 9)
+                p.kill()
                 p.wait()
-        return {"error": "timeout"}
+        return {"error": "timeout", "ranks": n_ranks}
     finally:
         for pname in PROTOCOLS:
             if os.path.exists(f"/dev/shm{shm}_{pname}"):
                 os.unlink(f"/dev/shm{shm}_{pname}")
     if any(p.returncode != 0 for p in procs):
         return {"error": [p.returncode for p in procs], "stderr": [e[-300:] for _, e in outs]}
-    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
-    return {"per_protocol_bytes": json.loads(lines[-1]),
-            "ranks": "2 processes, rank r on GPU r, fp32 sum; SIMPLE at 4 and 64 MiB, LL and LL128 at 4 MiB"}
+    lines = [json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]) for o, _ in outs]
+    r0 = lines[0]["results"]
+    exact_all = all(v["exact"] for ln in lines for proto in ln["results"].values() for v in proto.values())
+    return {"per_protocol_bytes": r0, "exact_all_ranks": exact_all, "gpus": [ln["gpu"] for ln in lines],
+            "ranks": f"{n_ranks} processes, rank r on GPU r, fp32 sum; SIMPLE at 4 and 64 MiB, LL and LL128 at 4 MiB; "
+                     "timings of rank 0"}
 
 
 if __name__ == "__main__":
-    if "--ring-only" in sys.argv:  # rehearsal of the process ring alone (any number of GPUs)
+    a = sys.argv
+    if "--ring-only" in a:  # rehearsal of the two-rank process ring alone (any number of GPUs)
         print(json.dumps(ring_processes()), flush=True)
         sys.exit(0)
-    if "--ring-rank" in sys.argv:
-        a = sys.argv
-        sys.exit(ring_rank(int(a[a.index("--ring-rank") + 1]), a[a.index("--shm") + 1],
-                           [int(v) for v in a[a.index("--counts") + 1].split(",")]))
+    if "--ring-all" in a:  # the process ring over the first N GPUs (bench.py at N >= 3)
+        n = int(a[a.index("--ring-all") + 1])
+        print(json.dumps(ring_processes(n, timeout_s=float(os.environ.get("NEXR_RING_ALL_TIMEOUT", "75")))),
+              flush=True)
+        sys.exit(0)
+    if "--ring-rank" in a:
+        sys.exit(ring_rank(int(a[a.index("--ring-rank") + 1]), int(a[a.index("--ranks") + 1]),
+                           a[a.index("--shm") + 1], [int(v) for v in a[a.index("--counts") + 1].split(",")]))
     sys.exit(main())
