@@ -540,6 +540,34 @@ def h2d_inclusive(pkg, cfg, reps: int = 3):
                                  "calling thread's copies into zero-copy slots)"}}
 
 
+def h2d_pinned_all_ranks(pkg, cfg, dist, device, reps: int = 3) -> dict:
+    """N > 1: every rank's C2 call on its own pinned host buffers (the zero-copy path over its own
+    PCIe link) at the same time, after a barrier — the host<->device-inclusive rate of the whole node,
+    where host memory and the links are shared (NUMA placement of pinned buffers is the
+    only coupling between GPUs, and only for this variant)."""
+    import torch
+
+    n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
+    srcs = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8).pin_memory() for _ in range(cfg["k"])]
+    dsts = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8).pin_memory() for _ in range(cfg["m"])]
+    for t in srcs:
+        t.random_(0, 255)
+    sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
+    pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, 0, host=True)  # warm
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, 0, host=True)
+    mine = time.perf_counter() - t0
+    per = dist.gather([mine], device)
+    slowest = max(p[0] for p in per)
+    alg = algorithmic_bytes(cfg)
+    del srcs, dsts
+    return {"value": round(dist.world * alg * reps / slowest / 1e9, 2), "unit": "GB/s",
+            "per_rank_gbs": [round(alg * reps / p[0] / 1e9, 2) for p in per], "ms_per_call_max": round(slowest / reps * 1e3, 3),
+            "path": "nexrReduceCopyHost on pinned host buffers (zero-copy over PCIe), every rank at once"}
+
+
 # ---- the two ways to drive N GPUs ---------------------------------------------------------------
 def main_ranks(args, cfg, pkg) -> dict | None:
     """One process per GPU (N=1 plain, or N>1 under torchrun): each rank times its own chunk."""
@@ -566,6 +594,10 @@ def main_ranks(args, cfg, pkg) -> dict | None:
             solo.append(dist.max(s, wl.dev))
             dist.barrier()
         c5 = c5_summary(dist.world, bytes_step, args.steps, max_s, solo[0], solo)
+    h2d_all = None
+    if dist.world > 1 and not args.no_h2d:
+        wl.free()
+        h2d_all = h2d_pinned_all_ranks(pkg, cfg, dist, wl.dev)
     result = None
     if dist.rank == 0:
         result = base_line(cfg, dist.world, args.steps, args.warmup, value, max_s,
@@ -588,6 +620,7 @@ def main_ranks(args, cfg, pkg) -> dict | None:
         else:
             result["per_gpu"] = per_gpu_summary(ranks, bytes_step, args.steps)
             result["c5"] = c5
+            result["h2d_inclusive"] = h2d_all
             if not args.no_xgmi:
                 result["xgmi_probe"] = xgmi_probe()
         print(json.dumps(result), flush=True)
