@@ -27,16 +27,31 @@ def test_bench_wrapper_reports_failures(monkeypatch):
     import bench
 
     class Boom:
+        pid = 999_999_999
         returncode = 3
-        stdout = ""
-        stderr = "boom"
 
-    monkeypatch.setattr(subprocess, "run", lambda *a, **k: Boom())
+        def __init__(self, *a, **k):
+            pass
+
+        def communicate(self, timeout=None):
+            return "", "boom"
+
+    monkeypatch.setattr(subprocess, "Popen", Boom)
     r = bench.xgmi_probe()
     assert r["error"] == "exit 3" and "boom" in r["stderr"]
 
-    def timeout(*a, **k):
-        raise subprocess.TimeoutExpired("x", 1)
+    killed = []
 
-    monkeypatch.setattr(subprocess, "run", timeout)
-    assert "TimeoutExpired" in bench.xgmi_probe()["error"]
+    class Hang(Boom):
+        calls = 0
+
+        def communicate(self, timeout=None):
+            Hang.calls += 1
+            if Hang.calls == 1:
+                raise subprocess.TimeoutExpired("x", 1)
+            return "", ""
+
+    monkeypatch.setattr(subprocess, "Popen", Hang)
+    monkeypatch.setattr(os, "killpg", lambda pid, sig: killed.append(pid))
+    assert "timeout" in bench.xgmi_probe()["error"]
+    assert killed == [Hang.pid]  # the probe's whole process group, not just the probe
