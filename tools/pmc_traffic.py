@@ -28,16 +28,26 @@ def per_dispatch(path, counter, kernel_substr):
     return vals
 
 
+def instantiation(cfg) -> str:
+    """The exact kernel instantiation a configuration launches, reduce_copy_kernel<DT, OP, K, POL, ...>
+    (the policy from the bytes the call streams, as pickPolicy in nexr_api.cpp), so that other launches
+    in the same process (C1's small ring steps, the extra configurations) never enter the median."""
+    streamed = (cfg["k"] + cfg["m"]) * cfg["buf_bytes"]
+    pol = 3 if streamed >= (512 << 20) else (1 if streamed >= (64 << 20) else 0)
+    return f"nexr::reduce_copy_kernel<{cfg['dt']}, {cfg['op']}, {cfg['k']}, {pol},"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--config", default="c2")
-    ap.add_argument("--kernel", default="nexr::reduce_copy_kernel")
+    ap.add_argument("--kernel", default=None, help="kernel-name substring (default: the config's instantiation)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     import bench
     cfg = bench.CONFIGS[a.config]
+    a.kernel = a.kernel or instantiation(cfg)
     f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
     if not f or not w:

@@ -12,7 +12,7 @@ for cfg in "$@"; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     name=${cfg}_$(echo $ctr | cut -d_ -f1 | tr A-Z a-z)
     timeout -s KILL 90 rocprofv3 --pmc $ctr --output-format csv -d "$out" -o "$name" -- \
-      python3 bench.py --config "$cfg" --steps 5 --warmup 2 --no-cpu --no-h2d > "$out/$name.log" 2>&1 || exit 1
+      python3 bench.py --config "$cfg" --steps 5 --warmup 2 --no-cpu --no-h2d --no-extra > "$out/$name.log" 2>&1 || exit 1
   done
   cp "$out/${cfg}_fetch_counter_collection.csv" "profiles/${tag}_${cfg}_pmc_fetch.csv" || exit 1
   cp "$out/${cfg}_write_counter_collection.csv" "profiles/${tag}_${cfg}_pmc_write.csv" || exit 1
