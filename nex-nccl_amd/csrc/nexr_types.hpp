@@ -222,8 +222,13 @@ struct Fold8 {
   __device__ static __forceinline__ void split(u32x4 x, u16x8& ev, u16x8& od) {
     const u16x8 h = bc<u16x8>(x);
     if constexpr (kHigh) {
+      // Min/Max fold each byte in the HIGH half of a 16-bit lane. The odd bytes already sit there;
+      // the even byte below them needs no masking: a 16-bit compare is decided by the high byte
+      // whenever the high bytes differ, and when they are equal either operand carries the same high
+      // byte, so the high byte of min/max(a, b) is min/max of the high bytes whatever the low bytes
+      // hold (signed or unsigned). Only the high bytes reach the result (join).
       ev = h << 8;
-      od = h & (u16x8)0xff00;
+      od = h;
     } else {
       ev = h;
       od = h >> 8;
