@@ -123,3 +123,26 @@ def test_k4_batch_at_the_c4_policy(nexr, oracle, dev):
     torch.cuda.synchronize()
     for o, e in zip(outs, expect):
         assert mg.canon_bytes(mg.I8, o.cpu().numpy()) == mg.canon_bytes(mg.I8, e)
+
+
+def test_k4_geometry_random_large_calls(nexr, oracle, dev):
+    """Twelve random K = 4 calls in both new regimes (13-140 MiB per buffer: 64-700 MiB streamed),
+    random datatype and op, random pointer phases (shared: the 2x512 / 1x1024 body; mixed: the
+    element path at the same geometry), M = 1 or 2, against the oracle."""
+    rng = np.random.default_rng(4242)
+    ops = [(mg.SUM, "sum"), (mg.PROD, "prod"), (mg.MINMAX, "min"), (mg.MINMAX, "max")]
+    for case in range(12):
+        dt = int(rng.choice([mg.I8, mg.U8, mg.I32, mg.U32, mg.I64, mg.F16, mg.F32, mg.F64, mg.BF16]))
+        op, name = ops[int(rng.integers(0, len(ops)))]
+        esz = np.dtype(mg.STORE[dt]).itemsize
+        n = int(rng.integers(13 * MIB, 140 * MIB)) // esz
+        shared = bool(rng.integers(0, 2))
+        ph = int(rng.integers(0, 16 // esz)) * esz
+        offs = [ph] * 5 if shared else [int(rng.integers(0, 16 // esz)) * esz for _ in range(5)]
+        arg = mg.minmax_arg(dt, name == "max") if op == mg.MINMAX else 0
+        srcs = mg.gen_inputs(dt, 4, n, 9100 + case, special=True)
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
+        got = _run(nexr, srcs, dt, op, arg, offs)
+        assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (case, mg.DT_NAMES[dt], name, n, offs)
+        del srcs, exp, got
+        torch.cuda.empty_cache()
