@@ -548,21 +548,32 @@ def h2d_pinned_all_ranks(pkg, cfg, dist, device, reps: int = 3) -> dict:
     import torch
 
     n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
-    srcs = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8).pin_memory() for _ in range(cfg["k"])]
-    dsts = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8).pin_memory() for _ in range(cfg["m"])]
-    for t in srcs:
-        t.random_(0, 255)
-    sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
-    pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, 0, host=True)  # warm
+    err = None
+    try:  # a rank that cannot pin its buffers still takes part in the barrier and the gather
+        srcs = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8).pin_memory() for _ in range(cfg["k"])]
+        dsts = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8).pin_memory() for _ in range(cfg["m"])]
+        for t in srcs:
+            t.random_(0, 255)
+        sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
+        pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, 0, host=True)  # warm
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        err = repr(e)[:200]
     dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, 0, host=True)
-    mine = time.perf_counter() - t0
+    mine = -1.0
+    if err is None:
+        try:
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, 0, host=True)
+            mine = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            err = repr(e)[:200]
     per = dist.gather([mine], device)
+    srcs = dsts = None
+    if any(p[0] <= 0 for p in per):
+        return {"error": err or "another rank failed", "per_rank_s": [p[0] for p in per]}
     slowest = max(p[0] for p in per)
     alg = algorithmic_bytes(cfg)
-    del srcs, dsts
     return {"value": round(dist.world * alg * reps / slowest / 1e9, 2), "unit": "GB/s",
             "per_rank_gbs": [round(alg * reps / p[0] / 1e9, 2) for p in per], "ms_per_call_max": round(slowest / reps * 1e3, 3),
             "path": "nexrReduceCopyHost on pinned host buffers (zero-copy over PCIe), every rank at once"}

@@ -84,3 +84,46 @@ def test_rank_stdout_is_only_the_json_line(tmp_path):
     outs = [p.communicate(timeout=120) for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
     assert [o for o, _ in outs] == ['{"rank": 0}\n', '{"rank": 1}\n']
+
+
+def _h2d_rank_main(rank, world, port, q, fail_rank):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    import bench
+    import torch
+
+    class FakePkg:  # stands in for the library: "copies" host buffers, or fails on one rank
+        def reduce_copy_ptrs(self, *a, **k):
+            if rank == fail_rank:
+                raise RuntimeError("pinning failed on this rank")
+
+    # torch pin_memory needs a GPU runtime; on CPU stand it in with the plain tensor
+    torch.Tensor.pin_memory = lambda self: self
+    d = bench.Dist("gloo")
+    cfg = dict(bench.CONFIGS["c2"])
+    cfg["buf_bytes"] = 1 << 20
+    res = bench.h2d_pinned_all_ranks(FakePkg(), cfg, d, None, reps=2)
+    d.close()
+    q.put((rank, res))
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_node_wide_h2d_leg_survives_a_failing_rank(fail_rank):
+    """bench.py's N > 1 host-inclusive leg: every rank joins the barrier and the gather even when one
+    rank fails, and the line records the failure instead of hanging or raising."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_h2d_rank_main, args=(r, 2, port, q, fail_rank)) for r in range(2)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=120) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    assert all(p.exitcode == 0 for p in ps)
+    if fail_rank < 0:
+        assert res[0]["value"] > 0 and len(res[0]["per_rank_gbs"]) == 2
+    else:
+        assert "error" in res[0] and "error" in res[1]
+        assert "pinning failed" in res[1]["error"]
