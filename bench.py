@@ -110,6 +110,10 @@ class Dist:
             if backend == "nccl":
                 import torch
                 kw["device_id"] = torch.device("cuda", local_device_index())
+            import datetime
+            # 10 minutes: longer than any leg a rank may wait through (rank 0's xGMI probes are bounded
+            # at ~4 minutes), far shorter than the 30-minute default should a rank ever hang
+            kw["timeout"] = datetime.timedelta(minutes=10)
             with stdout_to_stderr():  # gloo prints its "[Gloo] Rank r is connected to ..." lines on fd 1
                 dist.init_process_group(backend=backend, rank=self.rank, world_size=self.world, **kw)
                 dist.barrier()
