@@ -180,3 +180,15 @@ def test_bounded_probe_kills_its_whole_process_group(tmp_path):
     assert ok == {"a": 1}
     bad = bench._bounded([sys.executable, "-c", "import sys; sys.exit(3)"], 30.0)
     assert bad["error"] == "exit 3"
+
+
+def test_side_leg_records_failures():
+    """A failing leg after the headline's timed region lands in the line as an error, not a crash."""
+    import bench
+
+    def c1_ring():
+        raise RuntimeError("peer access refused")
+
+    r = bench.side_leg(c1_ring)
+    assert r["leg"] == "c1_ring" and "peer access refused" in r["error"]
+    assert bench.side_leg(lambda a, b: a + b, 2, 3) == 5
