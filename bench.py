@@ -299,8 +299,12 @@ def c1_ring(iters: int = 20) -> dict:
     ol = oracle.lib()
     cpu_fn = ctypes.cast(ol.oracle_reduce_copy_emulated_fn, ctypes.c_void_p).value
     out = {"workload": "fp32 sum all-reduce, 4 MiB per rank, 2 emulated ranks, ring SIMPLE, 1 channel"}
-    for name, mode, fn in (("device", ring.DEVICE_MEMORY, None), ("host_staged", ring.HOST_MEMORY, None),
-                           ("cpu_oracle", ring.HOST_MEMORY, cpu_fn)):
+    legs = (("device", ring.DEVICE_MEMORY, None, ring.PROTO_SIMPLE),
+            ("device_ll", ring.DEVICE_MEMORY, None, ring.PROTO_LL),
+            ("device_ll128", ring.DEVICE_MEMORY, None, ring.PROTO_LL128),
+            ("host_staged", ring.HOST_MEMORY, None, ring.PROTO_SIMPLE),
+            ("cpu_oracle", ring.HOST_MEMORY, cpu_fn, ring.PROTO_SIMPLE))
+    for name, mode, fn, proto in legs:
         if mode == ring.DEVICE_MEMORY:  # rank r's buffers on rank r's GPU (libnexr_ring: r mod visible)
             devs = [torch.device("cuda", r % torch.cuda.device_count()) for r in range(n)]
             send = [torch.from_numpy(v).to(d) for v, d in zip(x, devs)]
@@ -313,7 +317,7 @@ def c1_ring(iters: int = 20) -> dict:
         sp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in send]
         rp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in recv]
         reps = iters if fn is None else max(2, iters // 10)
-        with ring.RingComm(n, mode, 0, fn) as comm:
+        with ring.RingComm(n, mode, 0, fn, protocol=proto) as comm:
             comm.all_reduce(sp, rp, count, 7, 0)
             t0 = time.perf_counter()
             for _ in range(reps):
@@ -322,7 +326,8 @@ def c1_ring(iters: int = 20) -> dict:
         got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
         out[name] = {"ms_per_call": round(dt * 1e3, 3), "algbw_gbs": round(count * 4 / dt / 1e9, 2), "calls": reps,
                      "exact": all(np.array_equal(g, expect) for g in got)}
-    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); cpu_oracle runs the same schedule with the "
+    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_ll / device_ll128 run the same ring "
+                   "with the LL / LL128 protocol steps (SURVEY §8(f) #3) in place of SIMPLE; cpu_oracle runs the same schedule with the "
                    "reference's CPU execution of reduceCopy (oracle_reduce_copy_emulated_fn: 480 emulated threads, "
                    "Unroll 4) as its reduce-copy on host cores")
     return out

@@ -1129,8 +1129,8 @@ NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRec
   a.srcIsInput = srcIsInput ? 1 : 0;
   a.postOp = postOp ? 1 : 0;
   llSemantics(&datatype, &devRedOp, &a.srcIsInput, &a.postOp, &a.firstWins);
-  const uint64_t nPairs = (nElts * typeSize(datatype) + 15) / 16;
-  uint64_t grid = (nPairs + kBlock - 1) / kBlock;
+  const uint64_t nLines = (nElts * typeSize(datatype) + 7) / 8;
+  uint64_t grid = (nLines + kLLTileLines - 1) / kLLTileLines;
   if (grid > (1u << 20)) grid = 1u << 20;
   NEXR_HIP(launch_ll(datatype, a, devRedOp, (int)grid, (hipStream_t)stream));
   return nexrSuccess;
@@ -1178,7 +1178,7 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
   a.postOp = postOp ? 1 : 0;
   llSemantics(&datatype, &devRedOp, &a.srcIsInput, &a.postOp, &a.firstWins);
   const uint64_t nUnits = (nElts * typeSize(datatype) + kLL128SliceData - 1) / kLL128SliceData * 128;
-  uint64_t grid = (nUnits + kBlock - 1) / kBlock;
+  uint64_t grid = (nUnits + kLL128TileUnits - 1) / kLL128TileUnits;
   if (grid > (1u << 20)) grid = 1u << 20;
   NEXR_HIP(launch_ll128(datatype, a, devRedOp, (int)grid, (hipStream_t)stream));
   return nexrSuccess;

@@ -53,6 +53,13 @@ hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s)
 // Wire: 2 KiB slices of 16 x 128-B lines carrying 1920 data bytes; word 15 of every line is the flag.
 constexpr int kLL128SliceBytes = 2048;
 constexpr int kLL128SliceData = 1920;
+// Work per workgroup iteration (nexr_ll.hip): LL, kLLU sub-tiles of 2 * kBlock lines (8 data bytes
+// each); LL128, kLL128U sub-tiles of kBlock 16-byte wire units. 16 KiB of data or wire per tile.
+constexpr int kLLU = 4;
+constexpr int kLLSubLines = 2 * kBlock;
+constexpr int kLLTileLines = kLLU * kLLSubLines;
+constexpr int kLL128U = 4;
+constexpr int kLL128TileUnits = kLL128U * kBlock;
 struct LL128Params {
   const char* src;
   const char* recv[NEXR_MAX_SRCS];
