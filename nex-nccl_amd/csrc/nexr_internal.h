@@ -54,11 +54,17 @@ hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s)
 constexpr int kLL128SliceBytes = 2048;
 constexpr int kLL128SliceData = 1920;
 // Work per workgroup iteration (nexr_ll.hip): LL, kLLU sub-tiles of 2 * kBlock lines (8 data bytes
-// each); LL128, kLL128U sub-tiles of kBlock 16-byte wire units. 16 KiB of data or wire per tile.
-constexpr int kLLU = 4;
+// each); LL128, kLL128U sub-tiles of kBlock 16-byte wire units. One sub-tile (4 KiB of data or wire
+// per workgroup) is fastest at the protocols' step sizes, 32 KiB-4 MiB, by up to 1.8x over four, and
+// for LL at 64 MiB as well; four gain <= 10 % only for LL128 at 64 MiB (tools/ll_bits.hip,
+// profiles/r02s5_ll_bits.txt).
+#ifndef NEXR_LL_U  // overridable only by tuning harnesses (tools/ll_bits.hip)
+#define NEXR_LL_U 1
+#endif
+constexpr int kLLU = NEXR_LL_U;
 constexpr int kLLSubLines = 2 * kBlock;
 constexpr int kLLTileLines = kLLU * kLLSubLines;
-constexpr int kLL128U = 4;
+constexpr int kLL128U = NEXR_LL_U;
 constexpr int kLL128TileUnits = kLL128U * kBlock;
 struct LL128Params {
   const char* src;
