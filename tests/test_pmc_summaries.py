@@ -50,3 +50,18 @@ def test_traffic_tool_counts_only_the_configs_instantiation(tmp_path):
     d = json.load(open(out))
     assert d["dispatches"] == {"fetch_pass": 3, "write_pass": 3}
     assert d["traffic_over_algorithmic"] == 1.0
+
+
+def test_ll_step_traffic_summary_reproduces_from_the_committed_counters():
+    """profiles/r02s5_ll_pmc.txt is rebuilt from the committed counter collections by
+    tools/ll_prof_summary.py, and every LL / LL128 / SIMPLE step moves its algorithmic bytes once."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import ll_prof_summary
+    p = lambda n: os.path.join(ROOT, "profiles", n)  # noqa: E731
+    rows = ll_prof_summary.main(["--fetch", p("r02s5_ll_pmc_fetch.csv"), "--write", p("r02s5_ll_pmc_write.csv"),
+                                 "--rate", p("r02s5_ll_pmc_rate.jsonl")])
+    assert len(rows) == 15 and {r["proto"] for r in rows} == {"ll", "ll128", "simple"}
+    assert all(0.999 <= r["traffic_over_alg"] <= 1.02 for r in rows), rows
+    committed = open(p("r02s5_ll_pmc.txt")).read().split("\n")[1:]
+    for r in rows:
+        assert any(f"{r['read_bytes']:>13} {r['write_bytes']:>13}" in ln for ln in committed), r
