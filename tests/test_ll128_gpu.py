@@ -91,3 +91,11 @@ def test_ll128_stale_flag_times_out(nexr, oracle):
                            stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert int(status.item()) == 1
+
+
+def test_ll128_tile_boundaries(nexr, oracle):
+    """Sizes around the kernel's layout: one 1920-byte slice, a tile's two slices (3840 bytes), and
+    partial last lines and chunks, on int8 (byte-granular sizes) and fp32, misaligned user buffers too."""
+    for k, n in enumerate((1919, 1920, 1921, 1928, 3839, 3840, 3841, 5760, 7681)):
+        _run(nexr, oracle, mg.I8, mg.SUM, 0, False, "recvReduceCopySend", n, src_off=k % 3, dst_off=1, seed=k)
+        _run(nexr, oracle, mg.F32, mg.PROD, 0, False, "twoPeers", -(-n // 4), seed=50 + k)

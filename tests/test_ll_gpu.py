@@ -92,3 +92,14 @@ def test_ll_missing_flag_times_out_without_hanging(nexr, oracle):
     torch.cuda.synchronize()
     assert int(status.item()) == 1
     assert int(dst.count_nonzero()) == 0  # nothing written for lines that never became valid
+
+
+def test_ll_tile_boundaries(nexr, oracle):
+    """Sizes around the kernel's layout: a wave's 128 lines (lanes j and j + 64), a tile's 512 lines,
+    and partial last lines, on int8 (byte-granular sizes) and fp32, misaligned user buffers too."""
+    for k, lines in enumerate((63, 64, 65, 127, 128, 129, 511, 512, 513, 1025)):
+        for extra in (-3, 0):
+            n = lines * 8 + extra
+            _run(nexr, oracle, mg.I8, mg.SUM, 0, False, "recvReduceCopySend", n, src_off=k % 3, dst_off=1, seed=k)
+        _run(nexr, oracle, mg.F32, mg.MINMAX, mg.minmax_arg(mg.F32, True), False, "twoPeers", lines * 2 - 1,
+             seed=50 + k)
