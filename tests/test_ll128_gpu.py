@@ -99,3 +99,29 @@ def test_ll128_tile_boundaries(nexr, oracle):
     for k, n in enumerate((1919, 1920, 1921, 1928, 3839, 3840, 3841, 5760, 7681)):
         _run(nexr, oracle, mg.I8, mg.SUM, 0, False, "recvReduceCopySend", n, src_off=k % 3, dst_off=1, seed=k)
         _run(nexr, oracle, mg.F32, mg.PROD, 0, False, "twoPeers", -(-n // 4), seed=50 + k)
+
+
+def test_ll128_beyond_the_grid_cap(nexr):
+    """The launch caps the grid at 2^20 tiles of two slices (3,840 data bytes each) and the kernel
+    strides over the rest: a 2^32 + 12,345-byte uint8 step (past the cap), its wire written by a send
+    step and then reduced with a local buffer (dst = peer + src, checked against torch)."""
+    n = (1 << 32) + 12_345
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    peer = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    wire = torch.zeros(-(-n // 1920) * 2048, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    nexr.reduce_copy_ll128(peer.data_ptr(), [], [], 0, [wire.data_ptr()], [(1 << 40) + 5], n, mg.U8, mg.SUM, stream=s)
+    del peer
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    dst = torch.empty_like(src)
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    nexr.reduce_copy_ll128(src.data_ptr(), [wire.data_ptr()], [(1 << 40) + 5], dst.data_ptr(), [], [], n, mg.U8,
+                           mg.SUM, status=status.data_ptr(), timeout_us=2_000_000, stream=s)
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    g.manual_seed(4)
+    peer = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    assert torch.equal(dst, peer + src)
+    del peer, wire, src, dst
+    torch.cuda.empty_cache()

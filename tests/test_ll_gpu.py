@@ -103,3 +103,29 @@ def test_ll_tile_boundaries(nexr, oracle):
             _run(nexr, oracle, mg.I8, mg.SUM, 0, False, "recvReduceCopySend", n, src_off=k % 3, dst_off=1, seed=k)
         _run(nexr, oracle, mg.F32, mg.MINMAX, mg.minmax_arg(mg.F32, True), False, "twoPeers", lines * 2 - 1,
              seed=50 + k)
+
+
+def test_ll_beyond_the_grid_cap(nexr):
+    """The launch caps the grid at 2^20 tiles of 512 lines (4 GiB of data) and the kernel strides
+    over the rest: a 4 GiB + 12,345-byte uint8 step, its wire written by a send step and then reduced
+    with a local buffer (dst = peer + src, checked against torch)."""
+    n = (1 << 32) + 12_345
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    peer = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    wire = torch.zeros(((n + 7) // 8) * 16, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    nexr.reduce_copy_ll(peer.data_ptr(), [], [], 0, [wire.data_ptr()], [77], n, mg.U8, mg.SUM, stream=s)
+    del peer
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    dst = torch.empty_like(src)
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    nexr.reduce_copy_ll(src.data_ptr(), [wire.data_ptr()], [77], dst.data_ptr(), [], [], n, mg.U8, mg.SUM,
+                        status=status.data_ptr(), timeout_us=2_000_000, stream=s)
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    g.manual_seed(3)
+    peer = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    assert torch.equal(dst, peer + src)
+    del peer, wire, src, dst
+    torch.cuda.empty_cache()
