@@ -282,10 +282,14 @@ NEXR_API nexrResult_t nexrGetSemantics(int* semantics);
 /*
  * nexrQueryLaunch — diagnostics: the launch nexrReduceCopy would make for these pointers and this
  * size (no GPU work, no device needed; the same validation as nexrReduceCopy with devRedOp = Sum).
- * `generic` is 1 when the pointers share no 16-B phase and every element takes the scalar path;
- * otherwise [0, headElts) and the tail are edge elements and bodyPacks 16-B packs form the aligned
- * body. grid * block never exceeds 2^32 - 1 work items (HIP's launch limit); larger calls
- * grid-stride. policy: 0 plain, 1 non-temporal loads, 3 non-temporal loads and stores.
+ * [0, headElts) and the tail are edge elements (headElts brings dsts[0] to a 128-B boundary when its
+ * offset is a whole number of elements) and bodyPacks 16-B packs form the body, pack i being the 16
+ * bytes at offset 16 i of every buffer. `unaligned` is 1 when the pointers share no 16-B phase: the
+ * body then moves the misaligned buffers with unaligned 16-B accesses. `generic` (the per-element
+ * path of round 1) is always 0 and kept for the layout; `unaligned` sits in what was padding, so
+ * the struct's size and offsets are unchanged. grid * block never exceeds 2^32 - 1 work items
+ * (HIP's launch limit); larger calls grid-stride. policy: 0 plain, 1 non-temporal loads, 3
+ * non-temporal loads and stores.
  */
 typedef struct {
   uint32_t grid;
@@ -293,6 +297,7 @@ typedef struct {
   int packsPerLane;
   int policy;
   int generic;
+  int unaligned;
   uint64_t headElts;
   uint64_t bodyPacks;
 } nexrLaunchInfo;

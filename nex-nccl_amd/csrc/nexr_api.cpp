@@ -182,20 +182,24 @@ nexrResult_t validate(int nSrcs, const void* const* srcs, int nDsts, void* const
   return nexrSuccess;
 }
 
-// Split [0, nElts) into head edge / 16-B aligned body / tail edge (RCParams comment).
+// Split [0, nElts) into head edge / packed body / tail edge (RCParams comment). Pack i of the body
+// is the 16 contiguous bytes at offset 16 i of every buffer, at that buffer's own alignment: when all
+// pointers share a 16-B phase every access is aligned; otherwise the misaligned ones are unaligned
+// 16-B loads / stores (one instruction per lane on gfx950, no element-by-element path). The head
+// brings the first destination to a 128-B boundary when its offset is a whole number of elements, so
+// that each wave's 1 KiB store instruction writes whole 128-B lines: misaligned stores cost more than
+// misaligned loads (tools/misalign_rate.py).
+constexpr uintptr_t kLineBytes = 128;
 void planLayout(RCParams& p, int nSrcs, size_t esz) {
-  uintptr_t phase = (uintptr_t)p.src[0] & 15;
-  bool common = (phase % esz) == 0;
-  for (int s = 1; s < nSrcs && common; s++) common = (((uintptr_t)p.src[s]) & 15) == phase;
-  for (int d = 0; d < p.nDsts && common; d++) common = (((uintptr_t)p.dst[d]) & 15) == phase;
-  if (!common) {
-    p.generic = 1;
-    p.head = 0;
-    p.nPacks = 0;
-    return;
-  }
+  const uintptr_t phase16 = (uintptr_t)p.src[0] & 15;
+  bool common = (phase16 % esz) == 0;
+  for (int s = 1; s < nSrcs && common; s++) common = (((uintptr_t)p.src[s]) & 15) == phase16;
+  for (int d = 0; d < p.nDsts && common; d++) common = (((uintptr_t)p.dst[d]) & 15) == phase16;
   p.generic = 0;
-  uint64_t head = phase ? (16 - phase) / esz : 0;
+  p.unaligned = common ? 0 : 1;
+  uintptr_t phase = (uintptr_t)p.dst[0] & (kLineBytes - 1);
+  if (phase % esz) phase = 0;
+  uint64_t head = phase ? (kLineBytes - phase) / esz : 0;
   if (head > p.nElts) head = p.nElts;
   p.head = head;
   p.nPacks = (p.nElts - head) * esz / 16;
@@ -217,11 +221,11 @@ void fillParams(RCParams& p, int nSrcs, const void* const* srcs, int nDsts, void
   planLayout(p, nSrcs, esz);
 }
 
-// One-shot workgroups of one reduce-copy: one per B lane work items, a work item being an element
-// (generic path) or a U-pack group (packed path), with (U, B) = the kernel's geometry for (dt, K).
+// One-shot workgroups of one reduce-copy: one per B lane work items, a work item being a U-pack
+// group, with (U, B) = the kernel's geometry for (dt, K, policy).
 uint64_t workgroupsFor(const RCParams& p, int nSrcs, int dt, int pol) {
   const uint64_t u = (uint64_t)unroll_for(dt, nSrcs, pol), b = (uint64_t)block_for(dt, nSrcs, pol);
-  const uint64_t items = p.generic ? p.nElts : (p.nPacks + u - 1) / u;
+  const uint64_t items = (p.nPacks + u - 1) / u;  // >= 1 workgroup (pickGeometry) covers the edges
   return (items + b - 1) / b;
 }
 
@@ -885,9 +889,10 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
   if (r != nexrSuccess) return r;
   info->grid = (uint32_t)g.grid;
   info->block = block;
-  info->packsPerLane = p.generic ? 1 : unroll_for(datatype, nSrcs, pol);
+  info->packsPerLane = unroll_for(datatype, nSrcs, pol);
   info->policy = g.pol;
-  info->generic = p.generic;
+  info->generic = 0;
+  info->unaligned = p.unaligned;
   info->headElts = p.head;
   info->bodyPacks = p.nPacks;
   return nexrSuccess;

@@ -12,11 +12,13 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes per workgroup
 
 // Launch parameters of one reduce-copy, passed by value as the kernel argument.
 //
-// Element range layout (host computes it, see plan_layout in nexr_api.cpp):
-//   [0, head)                    edge elements before the first 16-B boundary (scalar path)
-//   [head, head + nPacks*EPP)    the aligned body: every src/dst pointer + head*esz is 16-B aligned
+// Element range layout (host computes it, see planLayout in nexr_api.cpp):
+//   [0, head)                    edge elements before dst[0]'s next 128-B boundary (scalar path)
+//   [head, head + nPacks*EPP)    the packed body: pack i = 16 contiguous bytes of every buffer
 //   [.., nElts)                  tail edge elements (scalar path)
-// When `generic` is set no common alignment exists and every element takes the scalar path.
+// When the pointers share a 16-B phase every body access is 16-B aligned; otherwise (`unaligned`)
+// the others are unaligned 16-B accesses. `generic` (every element on the scalar path) is no longer
+// used and stays 0.
 struct RCParams {
   const char* src[NEXR_MAX_SRCS];
   char* dst[NEXR_MAX_DSTS];
@@ -30,6 +32,7 @@ struct RCParams {
   int nPreOp;                   // pre-op applies to srcs[s] for s < nPreOp
   int postOp;
   int generic;
+  int unaligned;  // no common 16-B phase: body packs use unaligned 16-B accesses (diagnostics)
 };
 
 // Launch parameters of one LL-protocol step (nexr_ll.hip; reference src/device/prims_ll.h:218-283).

@@ -123,11 +123,7 @@ __device__ __forceinline__ void body(const RCParams& p, uint64_t bid, uint64_t n
   const uint64_t gid = bid * B + threadIdx.x;
   const uint64_t nthreads = nblk * B;
 
-  if (p.generic) {  // pointers share no 16-B phase: every element on the scalar path
-    for (uint64_t i = gid; i < p.nElts; i += nthreads) do_element<D, OP, K, IsMin>(src, dst, nDsts, f, i);
-    return;
-  }
-  // Edge elements before/after the aligned body: at most 2*(16/esz - 1) of them.
+  // Edge elements before/after the packed body: fewer than 128/esz + 16/esz of them.
   const uint64_t bodyElts = p.nPacks * T::EPP;
   const uint64_t head = p.head;
   const uint64_t tail = p.nElts - head - bodyElts;
@@ -136,7 +132,8 @@ __device__ __forceinline__ void body(const RCParams& p, uint64_t bid, uint64_t n
     do_element<D, OP, K, IsMin>(src, dst, nDsts, f, e);
   }
 
-  // Aligned body: base pointers advanced past the head edge.
+  // Packed body: base pointers advanced past the head edge. Pointers without the common 16-B phase
+  // are read / written with unaligned 16-B accesses (ld16 / st16 assume only byte alignment).
 #pragma unroll
   for (int s = 0; s < K; s++) src[s] += head * esz;
 #pragma unroll

@@ -181,18 +181,24 @@ template <> struct Ty<nexrBfloat16> {
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+// The reduce-copy's 16-B accesses assume byte alignment only: for 16-B aligned addresses the
+// instruction is the same global_load/store_dwordx4 (identical ISA), and for the rest gfx950 runs the
+// unaligned dwordx4 itself, at near the aligned rate (tools/misalign_rate.py).
+typedef u32x4 __attribute__((aligned(1))) u32x4_a1;
+typedef __attribute__((address_space(1))) const u32x4_a1 g_cu32x4_a1;
+typedef __attribute__((address_space(1))) u32x4_a1 g_u32x4_a1;
 
 // Cache policy POL: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
 enum { kPolPlain = 0, kPolNtLoad = 1, kPolNtStore = 2, kPolNt = 3 };
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const char* p) {
-  g_cu32x4* q = (g_cu32x4*)(p);
+  g_cu32x4_a1* q = (g_cu32x4_a1*)(p);
   if constexpr (POL & kPolNtLoad) return __builtin_nontemporal_load(q);
   else return *q;
 }
 template <int POL>
 __device__ __forceinline__ void st16(char* p, u32x4 v) {
-  g_u32x4* q = (g_u32x4*)(p);
+  g_u32x4_a1* q = (g_u32x4_a1*)(p);
   if constexpr (POL & kPolNtStore) __builtin_nontemporal_store(v, q);
   else *q = v;
 }

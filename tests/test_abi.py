@@ -158,23 +158,24 @@ def test_dev_red_op_full_padding_is_never_read(nexr):
 
 
 def test_query_launch_grid_respects_the_work_item_limit(nexr):
-    """Advisor r1: the grid cap must keep grid x block <= 2^32 - 1 (HIP's limit). A 2^32-element
-    generic-path call (pointers with mixed 16-B phases) needs ~2^32 work items; the launch must cap
-    the grid and grid-stride instead of failing."""
-    n = 1 << 32
-    # int8, K=2: mixed phases -> generic path, block 256
-    info = nexr.query_launch([0x1000, 0x2001], [0x3000], n, 0)
-    assert info.generic == 1 and info.block == 256
+    """Advisor r1: the grid cap must keep grid x block <= 2^32 - 1 (HIP's limit); a call that needs
+    more workgroups is capped and grid-strides instead of failing. Pointers with mixed 16-B phases
+    take the packed path too (unaligned 16-B accesses), never an element-per-work-item path."""
+    # int8, K=2, mixed phases: packed, unaligned; 1 TiB per buffer needs 2^32 workgroups of 256
+    info = nexr.query_launch([0x1000, 0x2001], [0x3000], 1 << 40, 0)
+    assert (info.generic, info.unaligned, info.block, info.packsPerLane) == (0, 1, 256, 4)
     assert info.grid * info.block <= 0xFFFFFFFF
     assert info.grid == 0xFFFFFFFF // 256
+    info = nexr.query_launch([0x1000, 0x2001], [0x3000], 1 << 32, 0)
+    assert info.unaligned == 1 and info.grid == (1 << 32) // 16 // 4 // 256
     # fp16 K=8 (block 1024): a 16 GiB body would need 2^20 workgroups -> under the 2^22 cap
     srcs = [0x10000 * (i + 1) for i in range(8)]
     info = nexr.query_launch(srcs, [0x100000], 8 << 30, 6)
     assert info.generic == 0 and info.block == 1024 and info.packsPerLane == 1
     assert info.grid == (8 << 30) * 2 // 16 // 1024 and info.grid * info.block <= 0xFFFFFFFF
-    # generic fp16 K=8 at 2^33 elements: capped at (2^32-1) // 1024
+    # fp16 K=8 with mixed phases at 2^33 elements: packed like the aligned call above
     info = nexr.query_launch([0x10000 * (i + 1) + (i & 1) * 2 for i in range(8)], [0x100000], 1 << 33, 6)
-    assert info.generic == 1 and info.grid == 0xFFFFFFFF // 1024
+    assert (info.generic, info.unaligned) == (0, 1) and info.grid == (1 << 34) // 16 // 1024
     # C2 geometry: 256 MiB fp32 K=2, U=4 packs per lane, one 16 KiB trip per workgroup, nt loads
     info = nexr.query_launch([0x10000000, 0x20000000], [0x30000000], 64 << 20, 7)
     assert (info.grid, info.block, info.packsPerLane, info.policy) == (16384, 256, 4, 3)
@@ -191,9 +192,21 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     for k in (3, 5):
         info = nexr.query_launch(k4[:3] + [0x50000000] * (k - 3), [0x60000000], 64 << 20, 7)
         assert (info.block, info.packsPerLane) == (256, 4)
-    # head/body/tail split for a shared 4-B phase
+    # head/body/tail split for a shared 4-B phase: the head brings dst0 to its next 128-B boundary
+    # (31 fp32 elements), then 17 packs, then 1 tail element
     info = nexr.query_launch([0x1004, 0x2004], [0x3004], 100, 7)
-    assert (info.generic, info.headElts, info.bodyPacks) == (0, 3, 24)
+    assert (info.generic, info.unaligned, info.headElts, info.bodyPacks) == (0, 0, 31, 17)
+    # mixed phases, dst0 already on a 128-B boundary: no head, 6 unaligned packs, 4 tail bytes
+    info = nexr.query_launch([0x1000, 0x2001], [0x3080], 100, 0)
+    assert (info.unaligned, info.headElts, info.bodyPacks) == (1, 0, 6)
+    # dst0 not on an element boundary (fp32 at an odd address): no head, all 16-B accesses unaligned
+    info = nexr.query_launch([0x1000, 0x2000], [0x3001], 100, 7)
+    assert (info.unaligned, info.headElts, info.bodyPacks) == (1, 0, 25)
+    # the diagnostics struct keeps round 1's size and offsets (`unaligned` took the padding)
+    import ctypes
+    L = nexr.LaunchInfo
+    assert ctypes.sizeof(L) == 40 and L.generic.offset == 16 and L.unaligned.offset == 20
+    assert L.headElts.offset == 24 and L.bodyPacks.offset == 32
     # validation as nexrReduceCopy; empty calls launch nothing
     with pytest.raises(nexr.NexrError):
         nexr.query_launch([0x1000, 0], [0x3000], 16, 7)

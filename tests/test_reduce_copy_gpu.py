@@ -112,7 +112,7 @@ def test_matches_oracle_all_ops_k_m(nexr, oracle, dt, dev):
 def test_unaligned_heads_tails_and_phases(nexr, oracle, dt, dev):
     esz = np.dtype(STORE_NP[dt]).itemsize
     rng = np.random.default_rng(100 + dt)
-    for trial in range(12):
+    for trial in range(16):
         k = int(rng.integers(1, 9))
         m = int(rng.integers(1, 4))
         n = int(rng.integers(1, 5000))
@@ -120,12 +120,17 @@ def test_unaligned_heads_tails_and_phases(nexr, oracle, dt, dev):
         if trial < 4:    # same 16-B phase everywhere: head/body/tail split
             ph = int(rng.integers(0, 16 // esz)) * esz
             so, do = [ph] * k, [ph] * m
-        elif trial < 8:  # different element-aligned phases: generic element path
+        elif trial < 8:  # different element-aligned phases: unaligned 16-B packs
             so = [int(rng.integers(0, 16 // esz)) * esz for _ in range(k)]
             do = [int(rng.integers(0, 16 // esz)) * esz for _ in range(m)]
-        else:            # not even element-aligned (the ABI requires no alignment)
+        elif trial < 12:  # not even element-aligned (the ABI requires no alignment)
             so = [int(rng.integers(0, 16)) for _ in range(k)]
             do = [int(rng.integers(0, 16)) for _ in range(m)]
+        else:            # anywhere in a 128-B line: the head that brings dst0 to a line boundary
+            so = [int(rng.integers(0, 128)) // (esz if trial < 14 else 1) * (esz if trial < 14 else 1)
+                  for _ in range(k)]
+            do = [int(rng.integers(0, 128)) // (esz if trial < 14 else 1) * (esz if trial < 14 else 1)
+                  for _ in range(m)]
         op, name = (mg.SUM, "sum") if trial % 2 == 0 else (mg.MINMAX, "max")
         arg = mg.minmax_arg(dt, True) if name == "max" else 0
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg)[0]
@@ -315,11 +320,10 @@ def test_buffers_larger_than_4gib(nexr, dev):
     torch.cuda.empty_cache()
 
 
-def test_generic_path_beyond_the_work_item_limit(nexr, dev):
-    """Advisor r1, on hardware: pointers with different 16-B phases take the per-element (generic)
-    path, one element per work item, so a call with more than 2^32 - 1 elements needs more work items
-    than HIP launches. The grid is capped at (2^32 - 1) / block (nexrQueryLaunch shows it) and the
-    kernel grid-strides over the rest: 2^32 + 4099 uint8 elements, src1 one byte off src0's phase."""
+def test_mixed_phases_beyond_4_gib(nexr, dev):
+    """Advisor r1, on hardware (round 1's per-element path for mixed 16-B phases needed more work items
+    than HIP launches here; round 2 moves such calls as unaligned 16-B packs): 2^32 + 4099 uint8
+    elements with src1 one byte off src0's phase, the grid within HIP's work-item limit."""
     n = (1 << 32) + 4099
     g = torch.Generator(device="cuda")
     g.manual_seed(9)
@@ -328,7 +332,7 @@ def test_generic_path_beyond_the_work_item_limit(nexr, dev):
     b = braw[1:]  # 16-B phase 1 against a's phase 0: no common alignment
     o = torch.empty_like(a)
     info = nexr.query_launch([a.data_ptr(), b.data_ptr()], [o.data_ptr()], n, nexr.DataType.Uint8)
-    assert info.generic == 1 and info.grid * info.block <= 0xFFFFFFFF < n
+    assert info.generic == 0 and info.unaligned == 1 and info.grid * info.block <= 0xFFFFFFFF < n
     nexr.reduce_copy([a, b], [o], nexr.DevRedOp.Sum, datatype=nexr.DataType.Uint8)
     torch.cuda.synchronize()
     assert torch.equal(o, a + b)
