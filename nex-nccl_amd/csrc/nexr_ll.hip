@@ -21,6 +21,8 @@
 namespace nexr {
 
 typedef __attribute__((address_space(1))) uint64_t g_u64;
+typedef uint64_t __attribute__((aligned(1))) u64_a1;  // user-buffer words at any alignment (nexr_types.hpp)
+typedef __attribute__((address_space(1))) u64_a1 g_u64_a1;
 
 __device__ __forceinline__ uint64_t ld_sys(const char* p) {
   return __hip_atomic_load((const g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -76,8 +78,8 @@ __device__ __forceinline__ bool poll_line(const char* p, uint32_t flag, const LL
 // The first n (<= 16) bytes at p as a zero-padded pack, and the reverse: byte accesses assembled in
 // registers (a variable-length memcpy into a register array would put the array on the stack).
 __device__ __forceinline__ u32x4 ld_partial(const char* p, uint64_t n) {
-  if (n == 8 && ((uintptr_t)p & 7) == 0) {  // an LL128 flag lane's half chunk
-    const uint64_t x = *(const g_u64*)p;
+  if (n == 8) {  // an LL128 flag lane's half chunk
+    const uint64_t x = *(const g_u64_a1*)p;
     return (u32x4){(uint32_t)x, (uint32_t)(x >> 32), 0u, 0u};
   }
   uint32_t w[4] = {0, 0, 0, 0};
@@ -87,8 +89,8 @@ __device__ __forceinline__ u32x4 ld_partial(const char* p, uint64_t n) {
   return (u32x4){w[0], w[1], w[2], w[3]};
 }
 __device__ __forceinline__ void st_partial(char* p, uint64_t n, u32x4 v) {
-  if (n == 8 && ((uintptr_t)p & 7) == 0) {
-    *(g_u64*)p = (uint64_t)v.y << 32 | v.x;
+  if (n == 8) {
+    *(g_u64_a1*)p = (uint64_t)v.y << 32 | v.x;
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -97,19 +99,20 @@ __device__ __forceinline__ void st_partial(char* p, uint64_t n, u32x4 v) {
     if ((uint64_t)k < n) p[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
 }
 
-// 8 data bytes of line l of a user buffer (fewer at its end; any alignment), and the reverse.
+// 8 data bytes of line l of a user buffer (fewer at its end; any alignment: unaligned 8-B
+// accesses, as the SIMPLE path's unaligned 16-B ones), and the reverse.
 __device__ __forceinline__ uint64_t ld_line(const char* p, uint64_t l, uint64_t nBytes) {
   const char* q = p + l * 8;
   const uint64_t v = nBytes - l * 8;
-  if (v >= 8 && ((uintptr_t)q & 7) == 0) return *(const g_u64*)q;
-  const u32x4 x = ld_partial(q, v < 8 ? v : 8);
+  if (v >= 8) return *(const g_u64_a1*)q;
+  const u32x4 x = ld_partial(q, v);
   return (uint64_t)x.y << 32 | x.x;
 }
 __device__ __forceinline__ void st_line(char* p, uint64_t l, uint64_t nBytes, uint64_t x) {
   char* q = p + l * 8;
   const uint64_t v = nBytes - l * 8;
-  if (v >= 8 && ((uintptr_t)q & 7) == 0) *(g_u64*)q = x;
-  else st_partial(q, v < 8 ? v : 8, (u32x4){(uint32_t)x, (uint32_t)(x >> 32), 0u, 0u});
+  if (v >= 8) *(g_u64_a1*)q = x;
+  else st_partial(q, v, (u32x4){(uint32_t)x, (uint32_t)(x >> 32), 0u, 0u});
 }
 
 // One tile = kLLU sub-tiles of 2 * kBlock lines. In a sub-tile, wave w owns lines [128w, 128w + 128)
@@ -309,7 +312,7 @@ __device__ __forceinline__ void ll128_tile(const LL128Params& a, uint64_t tile, 
     dOff[u] = dBase + off;
     d[u] = (u32x4)0u;
     if (a.src) {
-      if (valid[u] == 16 && (((uintptr_t)(a.src + dOff[u])) & 15) == 0) d[u] = *(const g_cu32x4*)(a.src + dOff[u]);
+      if (valid[u] == 16) d[u] = *(const g_cu32x4_a1*)(a.src + dOff[u]);
       else if (valid[u]) d[u] = ld_partial(a.src + dOff[u], valid[u]);
       if constexpr (OP == nexrDevPreMulSum) {
         if (a.srcIsInput) d[u] = bc<u32x4>(T::mul(bc<V>(d[u]), T::splat(a.redArg)));
@@ -366,7 +369,7 @@ __device__ __forceinline__ void ll128_tile(const LL128Params& a, uint64_t tile, 
 #pragma unroll
     for (int u = 0; u < kLL128U; u++) {
       if (!ok[u] || !valid[u]) continue;
-      if (valid[u] == 16 && (((uintptr_t)(a.dst + dOff[u])) & 15) == 0) *(g_u32x4*)(a.dst + dOff[u]) = d[u];
+      if (valid[u] == 16) *(g_u32x4_a1*)(a.dst + dOff[u]) = d[u];
       else st_partial(a.dst + dOff[u], valid[u], d[u]);
     }
   }
