@@ -470,3 +470,31 @@ def test_random_fuzz_against_oracle(nexr, oracle, dev):
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg, pre, post)[0]
         for o in run_gpu(nexr, srcs, m, dt, op, arg, pre, post, src_off=so, dst_off=do):
             assert same(dt, o, exp), (case, mg.DT_NAMES[dt], name, k, m, n, so, do)
+
+
+@pytest.mark.parametrize("offs", [(0, 4, 0), (4, 0, 12), (1, 3, 5), (0, 0, 1)])
+def test_large_misaligned_streams(nexr, dev, offs):
+    """256 MiB per buffer (768 MiB streamed: non-temporal loads and stores) with the sources and the
+    destination at the given byte offsets, element-aligned or not: the body's unaligned 16-B packs
+    under the streaming policy, checked bit for bit against torch's fp32 add, guard bytes intact."""
+    n = 64 << 20
+    nb = n * 4
+    g = torch.Generator(device="cuda")
+    g.manual_seed(sum(offs) + 5)
+    a = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    b = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    raw = [torch.full((nb + 256,), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    raw[0][offs[0]:offs[0] + nb] = a.view(torch.uint8)
+    raw[1][offs[1]:offs[1] + nb] = b.view(torch.uint8)
+    info = nexr.query_launch([raw[0].data_ptr() + offs[0], raw[1].data_ptr() + offs[1]],
+                             [raw[2].data_ptr() + offs[2]], n, nexr.DataType.Float32)
+    assert info.policy == 3 and info.unaligned == int(len({o % 16 for o in offs}) > 1)
+    nexr.reduce_copy_ptrs([raw[0].data_ptr() + offs[0], raw[1].data_ptr() + offs[1]], [raw[2].data_ptr() + offs[2]],
+                          n, nexr.DataType.Float32, nexr.DevRedOp.Sum,
+                          stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = raw[2][offs[2]:offs[2] + nb].clone().view(torch.float32)
+    assert torch.equal(out.view(torch.int32), (a + b).view(torch.int32))
+    assert bool((raw[2][:offs[2]] == 0x5A).all()) and bool((raw[2][offs[2] + nb:] == 0x5A).all())
+    del a, b, raw, out
+    torch.cuda.empty_cache()
