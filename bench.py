@@ -300,6 +300,7 @@ def c1_ring(iters: int = 20) -> dict:
     cpu_fn = ctypes.cast(ol.oracle_reduce_copy_emulated_fn, ctypes.c_void_p).value
     out = {"workload": "fp32 sum all-reduce, 4 MiB per rank, 2 emulated ranks, ring SIMPLE, 1 channel"}
     legs = (("device", ring.DEVICE_MEMORY, None, ring.PROTO_SIMPLE),
+            ("device_resident", ring.DEVICE_MEMORY, None, ring.PROTO_SIMPLE),
             ("device_ll", ring.DEVICE_MEMORY, None, ring.PROTO_LL),
             ("device_ll128", ring.DEVICE_MEMORY, None, ring.PROTO_LL128),
             ("host_staged", ring.HOST_MEMORY, None, ring.PROTO_SIMPLE),
@@ -317,16 +318,19 @@ def c1_ring(iters: int = 20) -> dict:
         sp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in send]
         rp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in recv]
         reps = iters if fn is None else max(2, iters // 10)
-        with ring.RingComm(n, mode, 0, fn, protocol=proto) as comm:
-            comm.all_reduce(sp, rp, count, 7, 0)
+        with ring.RingComm(n, mode, 0, fn, protocol=proto, timeout_ms=10000) as comm:
+            call = comm.all_reduce_resident if name == "device_resident" else comm.all_reduce
+            call(sp, rp, count, 7, 0)
             t0 = time.perf_counter()
             for _ in range(reps):
-                comm.all_reduce(sp, rp, count, 7, 0)
+                call(sp, rp, count, 7, 0)
             dt = (time.perf_counter() - t0) / reps
         got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
         out[name] = {"ms_per_call": round(dt * 1e3, 3), "algbw_gbs": round(count * 4 / dt / 1e9, 2), "calls": reps,
                      "exact": all(np.array_equal(g, expect) for g in got)}
-    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_ll / device_ll128 run the same ring "
+    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_resident runs the same schedule as one "
+                   "device-resident launch (nexrRingAllReduceResident: every rank's runRing inside the kernel, step "
+                   "counters in HBM) instead of one reduce-copy launch per slice; device_ll / device_ll128 run the same ring "
                    "with the LL / LL128 protocol steps (SURVEY §8(f) #3) in place of SIMPLE; cpu_oracle runs the same schedule with the "
                    "reference's CPU execution of reduceCopy (oracle_reduce_copy_emulated_fn: 480 emulated threads, "
                    "Unroll 4) as its reduce-copy on host cores")

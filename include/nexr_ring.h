@@ -90,6 +90,18 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* comm, const nexrRingCon
 NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op);
 
+/* ncclAllReduce (ring, SIMPLE) as ONE device-resident launch per GPU instead of one reduce-copy launch
+ * per slice: every rank's runRing (all_reduce.h:12-84) runs inside the kernel, its blocks waiting on
+ * step counters in HBM (waitPeer/postPeer, prims_simple.h:111-188) instead of the host sequencing
+ * steps. Same arguments, chunking, channel split and per-element results as nexrRingAllReduce.
+ * Requires memMode = device, protocol = SIMPLE, nRanks <= 16, and is nexrInvalidUsage under
+ * nexrSemanticsShipped. Each (rank, channel) runs as a team of workgroups (NEXR_RESIDENT_TEAM, default
+ * ~512 workgroups per GPU), each moving its own byte range of every FIFO slot with its own step
+ * counters. A step wait that exceeds timeoutMs fails the call (nexrInternalError) and marks the
+ * communicator broken. Blocks until every GPU's launch has finished. */
+NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t count, int datatype, int op);
+
 /* ncclReduceScatter: rank r's sendbuffs[r] holds nRanks*recvcount elements; recvbuffs[r] receives the
  * reduction of every rank's segment r (recvcount elements). */
 NEXR_API nexrResult_t nexrRingReduceScatter(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,

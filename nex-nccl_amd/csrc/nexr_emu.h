@@ -150,6 +150,12 @@ struct nexrRingComm {
   bool needHip = false;
   bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
   bool broken = false;
+  // Resident ring (nexrRingAllReduceResident), made by its first call: for every device hosting ranks
+  // (resDevs, in order of first appearance), the (channel, rank) connection table and the step-counter
+  // block in that device's memory, and a pinned, device-mapped status word.
+  std::vector<int> resDevs;
+  std::vector<void*> resTable, resCtr;
+  std::vector<uint32_t*> resStatus;
   // Process ranks: this process is rank `self` only.
   bool peer = false;
   int self = 0;

@@ -18,68 +18,13 @@
 //     to the result and is not reproduced.
 // The element arithmetic keeps the reference's left-fold order (acc is the first operand,
 // reduce_kernel.h:152-168) and rounds to T after every step.
-#include "nexr_types.hpp"
+#include "nexr_fold.hpp"
 
 #ifndef NEXR_DT
 #error "compile with -DNEXR_DT=<datatype>"
 #endif
 
 namespace nexr {
-
-template <int D, int OP, int K, bool IsMin>
-struct Fold {
-  using T = Ty<D>;
-  using V = typename T::V;
-  V factor[K];  // PreMulSum scalars, broadcast
-  int nPreOp;
-  bool post, canon;
-  uint64_t redArg;
-
-  __device__ Fold(const RCParams& p) {
-    nPreOp = p.nPreOp;
-    post = (OP == nexrDevSumPostDiv) && p.postOp;
-    redArg = p.redArg;
-    // ncclFromFloat runs whenever any arithmetic step ran (K>=2, or a pre-op on src0).
-    canon = (K >= 2) || (OP == nexrDevPreMulSum && p.nPreOp > 0);
-    if constexpr (OP == nexrDevPreMulSum) {
-#pragma unroll
-      for (int s = 0; s < K; s++) factor[s] = T::splat(p.pre[s]);
-    }
-  }
-  __device__ __forceinline__ V pre(V x, int s) const {
-    if constexpr (OP == nexrDevPreMulSum) {
-      if (s < nPreOp) return T::mul(x, factor[s]);  // Apply_PreOp<FuncPreMulSum> :498-518
-    }
-    return x;
-  }
-  // in[s] = the K loaded packs of one position
-  __device__ __forceinline__ u32x4 run(const u32x4 (&in)[K]) const {
-    if constexpr ((D == nexrInt8 || D == nexrUint8) && K >= 2 &&
-                  (OP == nexrDevSum || OP == nexrDevProd || OP == nexrDevMinMax)) {
-      using F = Fold8<OP, D == nexrInt8, IsMin>;  // two bytes per packed 16-bit instruction
-      u16x8 ae, ao;
-      F::split(in[0], ae, ao);
-#pragma unroll
-      for (int s = 1; s < K; s++) {
-        u16x8 e, o;
-        F::split(in[s], e, o);
-        ae = F::step(ae, e);
-        ao = F::step(ao, o);
-      }
-      return F::join(ae, ao);
-    }
-    V acc = pre(bc<V>(in[0]), 0);
-#pragma unroll
-    for (int s = 1; s < K; s++) acc = reduce_step<D, OP, IsMin>(acc, pre(bc<V>(in[s]), s));
-    if constexpr (OP == nexrDevSumPostDiv) {
-      if (post) acc = T::divide(acc, redArg);  // Apply_PostOp<FuncSumPostDiv> :520-539
-    }
-    if constexpr (D == nexrFloat16) {
-      if (canon) acc = T::canon(acc);
-    }
-    return bc<u32x4>(acc);
-  }
-};
 
 // One element through the same pack arithmetic (lanes other than 0 hold zeros and are dropped).
 // Byte-wise copies: the ABI allows pointers that are not even element-aligned.

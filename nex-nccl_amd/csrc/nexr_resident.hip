@@ -1,0 +1,335 @@
+// nexr_resident.hip — the ring all-reduce as ONE device-resident launch per GPU.
+//
+// What it runs is the reference's device kernel for ncclAllReduce with NCCL_ALGO_RING /
+// NCCL_PROTO_SIMPLE: runRing (src/device/all_reduce.h:12-84) over Primitives::genericOp
+// (src/device/prims_simple.h:190-330) with the FIFO credit protocol of waitPeer / postPeer
+// (:111-188): NCCL_STEPS = 8 slots of stepBytes per connection, a slice spans StepPerSlice steps, the
+// receiver waits for tail >= step + StepPerSlice, the sender for head + NCCL_STEPS >= step +
+// StepPerSlice, and each side posts its step once the slice is done. The host-sequenced ring in
+// nexr_ring.cpp runs the same schedule with one reduce-copy launch per slice; this file runs every
+// rank's whole schedule inside one launch, each rank's blocks waiting on the step counters in HBM
+// instead of the host waiting on streams.
+//
+// MI355X mapping:
+//   - a (rank, channel) is a TEAM of `team` workgroups, not one block: every FIFO slot's bytes are
+//     cut into `team` fixed runs of whole 16-byte packs, and workgroup g of a team moves the
+//     elements of every slice of its rank that fall in run g. Member g of rank r only ever consumes
+//     what member g of rank r-1 produced, into bytes only they touch, so each member runs the credit
+//     protocol on its own (tail, head) record and a team needs no barrier across workgroups: the
+//     reference's one-block-per-channel FIFO, replicated `team` times over disjoint byte ranges of
+//     each slot. What every element goes through — which rank reduces it at
+//     which step, operand order, rounding — is the reference's, so results equal the host ring's.
+//   - FIFO data moves with system-coherent 16-byte buffer accesses (sc0 sc1, as the LL steps'
+//     wire accesses, nexr_ll.hip): the consumer may sit on another XCD or another GPU, whose caches
+//     do not snoop the producer's writes; with every wave's accesses drained before the one-lane
+//     counter store, no L2 write-back or invalidate is needed per slice. User buffers use ordinary
+//     16-byte accesses.
+//   - step counters are 64-bit words, one record per member in its own 128-byte lines, written by
+//     one workgroup and polled by one other; every wait is bounded in time (s_memrealtime) and a
+//     timeout is reported in the device's status word, never a hang.
+#include "nexr_fold.hpp"
+#include "nexr_resident.h"
+
+namespace nexr {
+
+constexpr int kResU = 4;  // packs per lane per pass (the SIMPLE kernel's default unroll)
+constexpr int kResBits = 17;  // raw_buffer aux bits: sc0 (bit 0) | sc1 (bit 4), system coherence
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t res_rsrc(const char* base, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 fifo_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return bc<u32x4>(__builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kResBits));
+}
+__device__ __forceinline__ void fifo_st(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kResBits);
+}
+typedef __attribute__((address_space(1))) uint64_t g_u64;
+__device__ __forceinline__ uint64_t ctr_ld(const char* p) {
+  return __hip_atomic_load((const g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void ctr_st(char* p, uint64_t v) {
+  __hip_atomic_store((g_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Every vector memory access of this wave complete (stores acknowledged, loads returned). Inline asm,
+// so that no compiler pass can drop it (MI355X_MICROARCH.md, "Compiler hazard").
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ int64_t imin(int64_t x, int64_t y) { return x < y ? x : y; }
+__device__ __forceinline__ int64_t imax(int64_t x, int64_t y) { return x > y ? x : y; }
+__device__ __forceinline__ int64_t divUp64(int64_t x, int64_t y) { return (x + y - 1) / y; }
+
+struct ResShared {
+  uint64_t recvStep, sendStep;
+  int ok;
+};
+
+// The first n (< 16) bytes at p as a zero-padded pack, and the reverse.
+__device__ __forceinline__ u32x4 ld_bytes(const char* p, uint32_t n) {
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if ((uint32_t)k < n) w[k >> 2] |= (uint32_t)(uint8_t)p[k] << (8 * (k & 3));
+  return (u32x4){w[0], w[1], w[2], w[3]};
+}
+__device__ __forceinline__ void st_bytes(char* p, uint32_t n, u32x4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if ((uint32_t)k < n) p[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+// One workgroup's piece of a slice: srcs = [user src if US] + [recv FIFO if R], dsts = [user dst if
+// UD] + [send FIFO if S] (genericOp's order, prims_simple.h:131-132, :238-242), `bytes` bytes.
+// FIFO pieces start 16-byte aligned and own their slot up to the next 16 bytes, so a partial last
+// pack moves whole there; user buffers get exactly their bytes.
+template <int D, int OP, bool IsMin, bool US, bool R, bool UD, bool S>
+__device__ __forceinline__ void piece(const char* usrc, const char* rfifo, char* udst, char* sfifo, uint64_t bytes,
+                                      const Fold<D, OP, (int)US + (int)R, IsMin>& f) {
+  constexpr int K = (int)US + (int)R;
+  const uint64_t rbytes = (bytes + 15) & ~15ull;
+  const __amdgpu_buffer_rsrc_t rr = res_rsrc(rfifo, R ? rbytes : 0);
+  const __amdgpu_buffer_rsrc_t sr = res_rsrc(sfifo, S ? rbytes : 0);
+  const uint64_t nFull = bytes / 16;
+  constexpr uint64_t kPass = (uint64_t)kBlock * kResU;
+  uint64_t base = 0;
+  for (; base + kPass <= nFull; base += kPass) {
+    u32x4 in[kResU][K];
+#pragma unroll
+    for (int u = 0; u < kResU; u++) {
+      const uint64_t j = base + u * kBlock + threadIdx.x;
+      if constexpr (US) in[u][0] = ld16<kPolPlain>(usrc + j * 16);
+      if constexpr (R) in[u][K - 1] = fifo_ld(rr, (uint32_t)(j * 16));
+    }
+#pragma unroll
+    for (int u = 0; u < kResU; u++) {
+      const uint64_t j = base + u * kBlock + threadIdx.x;
+      const u32x4 out = f.run(in[u]);
+      if constexpr (UD) st16<kPolPlain>(udst + j * 16, out);
+      if constexpr (S) fifo_st(sr, (uint32_t)(j * 16), out);
+    }
+  }
+  const uint64_t nPacks = (bytes + 15) / 16;
+  for (uint64_t j = base + threadIdx.x; j < nPacks; j += kBlock) {
+    const uint32_t valid = j < nFull ? 16u : (uint32_t)(bytes - nFull * 16);
+    u32x4 in[K];
+    if constexpr (US) in[0] = valid == 16 ? ld16<kPolPlain>(usrc + j * 16) : ld_bytes(usrc + j * 16, valid);
+    if constexpr (R) in[K - 1] = fifo_ld(rr, (uint32_t)(j * 16));
+    const u32x4 out = f.run(in);
+    if constexpr (UD) {
+      if (valid == 16) st16<kPolPlain>(udst + j * 16, out);
+      else st_bytes(udst + j * 16, valid, out);
+    }
+    if constexpr (S) fifo_st(sr, (uint32_t)(j * 16), out);
+  }
+}
+
+// One rank's Primitives for one (channel, team member): step counters, connections, user buffers.
+template <int D, int OP, bool IsMin>
+struct ResPrims {
+  static constexpr int esz = 16 / Ty<D>::EPP;
+  const ResParams& a;
+  const char* input;
+  char* output;
+  char* recvFifo;
+  char* sendFifo;
+  char* recvTail;  // this member's record on this rank's device
+  char* recvHead;
+  char* sendTail;  // this member's record on the next rank's device
+  char* sendHead;
+  uint64_t recvStep, sendStep;
+  int member;
+  ResShared* sh;  // the wait's outcome and the attached steps, broadcast from thread 0
+
+  // waitPeer's spin (prims_simple.h:116-123), thread 0 only, bounded like checkAbort
+  // (primitives.h:142-156): false after a timeout (status set) or once another workgroup's timeout
+  // is visible in the status word.
+  __device__ bool wait_ge(const char* p, uint64_t target) const {
+    uint64_t t0 = 0;
+    for (uint32_t spins = 0;; spins++) {
+      if (ctr_ld(p) >= target) return true;
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (!t0) t0 = now;
+      if ((spins & 255) == 255 && __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+        return false;
+      if (now - t0 > a.timeoutTicks) {
+        __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+
+  // loadRecvConn / loadSendConn (prims_simple.h:512-517, :557-558): steps resume from the previous
+  // collective's, rounded up to SlicePerChunk * StepPerSlice, the receiver publishing its rounded step.
+  __device__ void attach() {
+    if (threadIdx.x == 0) {
+      const uint64_t cs = (uint64_t)(a.stepPerSlice * a.slicePerChunk);
+      const uint64_t rs = (ctr_ld(recvHead) + cs - 1) / cs * cs;
+      const uint64_t ss = (ctr_ld(sendTail) + cs - 1) / cs * cs;
+      ctr_st(recvHead, rs);
+      sh->recvStep = rs;
+      sh->sendStep = ss;
+    }
+    __syncthreads();
+    recvStep = sh->recvStep;
+    sendStep = sh->sendStep;
+    __syncthreads();
+  }
+
+  // genericOp<0, 0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330) for this member's pieces.
+  template <bool US, bool R, bool UD, bool S>
+  __device__ bool op(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
+    constexpr int K = (int)US + (int)R;
+    RCParams p{};
+    p.pre[0] = a.redArg;
+    p.redArg = a.redArg;
+    p.nPreOp = US ? 1 : 0;  // PreOpSrcs = SrcBuf == Input (prims_simple.h:279-280)
+    p.postOp = postOp ? 1 : 0;
+    const Fold<D, OP, K, IsMin> f(p);
+    nelem = nelem < 0 ? 0 : nelem;
+    int64_t sliceSize = a.stepElems * a.stepPerSlice;
+    sliceSize = imax(divUp64(nelem, 16 * (int64_t)a.slicePerChunk) * 16, sliceSize / 32);
+    int64_t offset = 0;
+    for (int slice = 0; slice < a.slicePerChunk; slice++) {
+      sliceSize = imin(sliceSize, nelem - offset);
+      if (sliceSize < 0) sliceSize = 0;
+      if (threadIdx.x == 0) {
+        bool ok = true;
+        if (R) ok = wait_ge(recvTail, recvStep + a.stepPerSlice);
+        if (ok && S && sendStep + a.stepPerSlice > 8) ok = wait_ge(sendHead, sendStep + a.stepPerSlice - 8);
+        sh->ok = ok ? 1 : 0;
+      }
+      __syncthreads();  // the other waves load the handed-off bytes only behind the poll
+      if (!sh->ok) return false;
+      // This member's piece of the slice. Pieces sit on a grid fixed for the call — the largest
+      // slice (StepPerSlice steps) cut into `team` runs of whole 16-byte packs — so that member g
+      // always owns the same bytes of every FIFO slot: its credits then cover exactly the bytes it
+      // writes, whatever size the slice that last used the slot had. A smaller slice leaves the
+      // high members idle.
+      constexpr int64_t epp = 16 / esz;
+      const int64_t per = divUp64(divUp64(a.stepElems * a.stepPerSlice, a.team), epp) * epp;
+      const int64_t lo = imin(sliceSize, per * member), hi = imin(sliceSize, lo + per);
+      if (hi > lo && K > 0 && ((int)UD + (int)S) > 0) {
+        const uint64_t slotOff = (uint64_t)lo * esz;
+        piece<D, OP, IsMin, US, R, UD, S>(
+            US ? input + (srcIx + offset + lo) * esz : nullptr,
+            R ? recvFifo + (recvStep % 8) * a.stepBytes + slotOff : nullptr,
+            UD ? output + (dstIx + offset + lo) * esz : nullptr,
+            S ? sendFifo + (sendStep % 8) * a.stepBytes + slotOff : nullptr, (uint64_t)(hi - lo) * esz, f);
+      }
+      // postPeer (prims_simple.h:177-188): every wave's FIFO stores acknowledged and FIFO loads
+      // returned, then one lane posts for the workgroup. FIFO bytes are written and read only with
+      // system-coherent accesses, so no cache write-back or invalidate is needed (the hand-off form
+      // "sc1 stores and loads both sides" of MI355X_MICROARCH.md, Guideline 16).
+      drain();
+      __syncthreads();
+      if (R) recvStep += a.stepPerSlice;
+      if (S) sendStep += a.stepPerSlice;
+      if (threadIdx.x == 0) {
+        if (R) ctr_st(recvHead, recvStep);
+        if (S) ctr_st(sendTail, sendStep);
+      }
+      offset += sliceSize;
+    }
+    return true;
+  }
+};
+
+// runRing for ncclAllReduce (all_reduce.h:12-84), one rank's view of one channel part.
+template <int D, int OP, bool IsMin>
+__device__ void run_ring(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
+  const int nranks = p.a.nRanks;
+  int64_t chunkCount = p.a.chunkCount;
+  const int64_t loopCount = nranks * chunkCount;
+  constexpr int64_t epp = 16 / ResPrims<D, OP, IsMin>::esz;
+  auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
+  for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += loopCount) {
+    const int64_t remCount = partCount - elemOffset;
+    if (remCount < loopCount) chunkCount = ((remCount + nranks - 1) / nranks + epp - 1) / epp * epp;
+    auto at = [&](int chunk, int64_t* offset) {
+      const int64_t chunkOffset = chunk * chunkCount;
+      *offset = partOffset + elemOffset + chunkOffset;
+      return imin(chunkCount, remCount - chunkOffset);
+    };
+    int64_t offset, nelem;
+    nelem = at(modRanks(rank + nranks - 1), &offset);  // step 0: push data to the next rank
+    if (!p.template op<true, false, false, true>(offset, -1, nelem, false)) return;
+    for (int j = 2; j < nranks; ++j) {  // k-2 steps: reduce and copy to the next rank
+      nelem = at(modRanks(rank + nranks - j), &offset);
+      if (!p.template op<true, true, false, true>(offset, -1, nelem, false)) return;
+    }
+    nelem = at(rank, &offset);  // step k-1: reduce this chunk -> final result, stored and pushed
+    if (!p.template op<true, true, true, true>(offset, offset, nelem, true)) return;
+    for (int j = 1; j < nranks - 1; ++j) {  // k-2 steps: copy to the next rank
+      nelem = at(modRanks(rank + nranks - j), &offset);
+      if (!p.template op<false, true, true, true>(-1, offset, nelem, false)) return;
+    }
+    nelem = at(modRanks(rank + 1), &offset);  // final copy from the FIFO to the output
+    if (!p.template op<false, true, true, false>(-1, offset, nelem, false)) return;
+  }
+}
+
+template <int D, int OP, bool IsMin>
+__global__ __launch_bounds__(kBlock) void ring_allreduce_resident(ResParams a) {
+  __shared__ ResShared sh;
+  const int member = blockIdx.x % a.team;
+  const int part = (blockIdx.x / a.team) % a.nParts;
+  const int rank = a.rankOf[blockIdx.x / (a.team * a.nParts)];
+  const ResConn& c = a.conns[a.partChannel[part] * a.nRanks + rank];
+  ResPrims<D, OP, IsMin> p{a};
+  p.input = a.input[rank];
+  p.output = a.output[rank];
+  p.recvFifo = c.recvFifo;
+  p.sendFifo = c.sendFifo;
+  p.recvTail = c.recvCtr + (size_t)member * kResCtrBytes;
+  p.recvHead = p.recvTail + kResHeadOff;
+  p.sendTail = c.sendCtr + (size_t)member * kResCtrBytes;
+  p.sendHead = p.sendTail + kResHeadOff;
+  p.member = member;
+  p.sh = &sh;
+  p.attach();
+  run_ring(p, rank, a.partOffset[part], a.partCount[part]);
+}
+
+template <int D, int OP>
+static hipError_t launch_op(const ResParams& p, int grid, hipStream_t s) {
+  const void* fn = (const void*)&ring_allreduce_resident<D, OP, false>;
+  if constexpr (OP == nexrDevMinMax) {
+    if ((p.redArg & 1) == 0) fn = (const void*)&ring_allreduce_resident<D, OP, true>;  // isMin, reduce_kernel.h:64
+  }
+  void* args[] = {const_cast<ResParams*>(&p)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+}
+
+template <int D>
+static hipError_t launch_dt(int op, const ResParams& p, int grid, hipStream_t s) {
+  switch (op) {
+    case nexrDevSum: return launch_op<D, nexrDevSum>(p, grid, s);
+    case nexrDevProd: return launch_op<D, nexrDevProd>(p, grid, s);
+    case nexrDevMinMax: return launch_op<D, nexrDevMinMax>(p, grid, s);
+    case nexrDevPreMulSum: return launch_op<D, nexrDevPreMulSum>(p, grid, s);
+    case nexrDevSumPostDiv:
+      if constexpr (Ty<D>::kIsInt) return launch_op<D, nexrDevSumPostDiv>(p, grid, s);
+      break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_resident(int dt, int op, const ResParams& p, int grid, hipStream_t s) {
+  switch (dt) {
+    case nexrInt8: return launch_dt<nexrInt8>(op, p, grid, s);
+    case nexrUint8: return launch_dt<nexrUint8>(op, p, grid, s);
+    case nexrInt32: return launch_dt<nexrInt32>(op, p, grid, s);
+    case nexrUint32: return launch_dt<nexrUint32>(op, p, grid, s);
+    case nexrInt64: return launch_dt<nexrInt64>(op, p, grid, s);
+    case nexrUint64: return launch_dt<nexrUint64>(op, p, grid, s);
+    case nexrFloat16: return launch_dt<nexrFloat16>(op, p, grid, s);
+    case nexrFloat32: return launch_dt<nexrFloat32>(op, p, grid, s);
+    case nexrFloat64: return launch_dt<nexrFloat64>(op, p, grid, s);
+    case nexrBfloat16: return launch_dt<nexrBfloat16>(op, p, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace nexr

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include "nexr_emu.h"
+#include "nexr_resident.h"
 
 namespace nexr_emu {
 
@@ -680,9 +681,171 @@ bool needsHip(const nexrRingConfig& cfg) {
          (cfg.protocol == nexrRingProtoLL && !cfg.llFn) || (cfg.protocol == nexrRingProtoLL128 && !cfg.ll128Fn);
 }
 
+// ---- resident ring (nexr_resident.hip) ----------------------------------------------------------
+void freeResident(nexrRingComm* c) {
+  for (size_t i = 0; i < c->resDevs.size(); i++) {
+    (void)hipSetDevice(c->resDevs[i]);
+    if (c->resTable[i]) (void)hipFree(c->resTable[i]);
+    if (c->resCtr[i]) (void)hipFree(c->resCtr[i]);
+    if (c->resStatus[i]) (void)hipHostFree(c->resStatus[i]);
+  }
+  c->resDevs.clear();
+  c->resTable.clear();
+  c->resCtr.clear();
+  c->resStatus.clear();
+}
+
+int resDevIndex(const nexrRingComm* c, int rank) {
+  for (size_t i = 0; i < c->resDevs.size(); i++)
+    if (c->resDevs[i] == c->devices[rank]) return (int)i;
+  return -1;
+}
+
+// First call: per device, a zeroed step-counter block with one record per (channel, rank, team
+// member) for the ranks it hosts, a status word, and the (channel, rank) connection table.
+nexrResult_t ensureResident(nexrRingComm* c) {
+  if (!c->resDevs.empty()) return nexrSuccess;
+  const int n = c->cfg.nRanks, nCh = c->cfg.nChannels;
+  for (int r = 0; r < n; r++)
+    if (std::find(c->resDevs.begin(), c->resDevs.end(), c->devices[r]) == c->resDevs.end())
+      c->resDevs.push_back(c->devices[r]);
+  const size_t nd = c->resDevs.size();
+  c->resTable.assign(nd, nullptr);
+  c->resCtr.assign(nd, nullptr);
+  c->resStatus.assign(nd, nullptr);
+  const size_t ctrBytes = (size_t)nCh * n * nexr::kResMaxTeam * nexr::kResCtrBytes;
+  for (size_t i = 0; i < nd; i++) {
+    if (hipSetDevice(c->resDevs[i]) != hipSuccess || hipMalloc(&c->resCtr[i], ctrBytes) != hipSuccess ||
+        hipMemset(c->resCtr[i], 0, ctrBytes) != hipSuccess ||
+        hipHostMalloc((void**)&c->resStatus[i], sizeof(uint32_t), hipHostMallocMapped | hipHostMallocPortable) !=
+            hipSuccess ||
+        hipMalloc(&c->resTable[i], sizeof(nexr::ResConn) * nCh * n) != hipSuccess) {
+      freeResident(c);
+      return nexrUnhandledCudaError;
+    }
+  }
+  std::vector<nexr::ResConn> table((size_t)nCh * n);
+  for (int ch = 0; ch < nCh; ch++) {
+    nexrRingComm* ck = channelComm(c, ch);
+    for (int r = 0; r < n; r++) {
+      const int nx = (r + 1) % n;
+      auto rec = [&](int rank) {
+        return (char*)c->resCtr[resDevIndex(c, rank)] +
+               ((size_t)(ch * n + rank) * nexr::kResMaxTeam) * nexr::kResCtrBytes;
+      };
+      table[(size_t)ch * n + r] = {ck->conns[r]->fifo, ck->conns[nx]->fifo, rec(r), rec(nx)};
+    }
+  }
+  for (size_t i = 0; i < nd; i++) {
+    *c->resStatus[i] = 0;
+    if (hipSetDevice(c->resDevs[i]) != hipSuccess ||
+        hipMemcpy(c->resTable[i], table.data(), sizeof(nexr::ResConn) * table.size(), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      freeResident(c);
+      return nexrUnhandledCudaError;
+    }
+  }
+  return nexrSuccess;
+}
+
+// Workgroups per (rank, channel): NEXR_RESIDENT_TEAM, else as many as give every member at least
+// 16 KiB of a full slice (StepPerSlice steps), at most about 512 workgroups on the busiest device (two
+// per CU) and at most kResMaxTeam. Measured on MI355X (tools/resident_time.py, 2 ranks, 256 MiB):
+// 16 KiB pieces beat 8 KiB ones (0.89 vs 1.03 ms on one channel) and 32/64 KiB ones at 4 channels.
+int residentTeam(int ranksOnDevice, int nParts, size_t sliceBytes) {
+  static const long env = [] {
+    const char* v = getenv("NEXR_RESIDENT_TEAM");
+    return v && *v ? strtol(v, nullptr, 0) : 0l;
+  }();
+  long t = env > 0 ? env
+                   : std::min<long>((long)(sliceBytes / (16 << 10)), 512 / std::max(1, ranksOnDevice * nParts));
+  return (int)std::max(1l, std::min<long>(t, nexr::kResMaxTeam));
+}
+
+nexrResult_t residentAllReduce(nexrRingComm* c, const void* const* sendbuffs, void* const* recvbuffs, size_t count,
+                               int datatype, int op) {
+  if (!c || c->peer) return nexrInvalidArgument;
+  if (c->cfg.memMode != nexrRingDeviceMemory || c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
+  int sem = nexrSemanticsNccl;
+  if (nexrGetSemantics(&sem) != nexrSuccess || sem == nexrSemanticsShipped) return nexrInvalidUsage;
+  size_t esz;
+  nexrDevRedOpFull red;
+  nexrResult_t r = prepare(c, datatype, op, &esz, &red);
+  if (r != nexrSuccess) return r;
+  const int n = c->cfg.nRanks;
+  if (!sendbuffs || !recvbuffs) return nexrInvalidArgument;
+  for (int i = 0; i < n; i++)
+    if (!sendbuffs[i] || !recvbuffs[i]) return nexrInvalidArgument;
+  if (count == 0) return nexrSuccess;
+  if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
+  if (n > nexr::kResMaxRanks) return nexrInvalidUsage;
+  // The fork's dispatch runs signed Min/Max on the unsigned kernel (generate.py:128-136).
+  int kdt = datatype;
+  if (sem == nexrSemanticsFork && red.op == nexrDevMinMax)
+    kdt = datatype == nexrInt8 ? nexrUint8 : datatype == nexrInt32 ? nexrUint32 : datatype == nexrInt64 ? nexrUint64 : datatype;
+  r = ensureResident(c);
+  if (r != nexrSuccess) return r;
+  const Geom g = kGeomRing;
+  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, /*ncclFuncAllReduce*/ 2);
+  nexr::ResParams a{};
+  a.nRanks = n;
+  a.nParts = (int)parts.size();
+  for (size_t i = 0; i < parts.size(); i++) {
+    a.partOffset[i] = parts[i].offset;
+    a.partCount[i] = parts[i].count;
+    a.partChannel[i] = parts[i].channel;
+  }
+  a.chunkCount = chunkElems(c, g, esz, false, 0);
+  a.stepElems = (int64_t)(c->stepBytes / esz);
+  a.stepBytes = c->stepBytes;
+  a.stepPerSlice = g.sliceSteps;
+  a.slicePerChunk = g.chunkSteps / g.sliceSteps;
+  a.redArg = red.scalarArg;
+  a.timeoutTicks = (uint64_t)(c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 100000ull;  // 100 MHz
+  for (int i = 0; i < n; i++) {
+    a.input[i] = (const char*)sendbuffs[i];
+    a.output[i] = (char*)recvbuffs[i];
+  }
+  int busiest = 0;
+  std::vector<std::vector<int>> onDev(c->resDevs.size());
+  for (int i = 0; i < n; i++) onDev[resDevIndex(c, i)].push_back(i);
+  for (const auto& v : onDev) busiest = std::max(busiest, (int)v.size());
+  a.team = residentTeam(busiest, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
+  // Every workgroup of a device's grid must be resident at once (a rank's blocks wait on others):
+  // at most four 256-lane workgroups per CU.
+  if ((long)busiest * a.nParts * a.team > 1024) return nexrInvalidUsage;
+  std::vector<hipStream_t> used;
+  for (size_t d = 0; d < onDev.size() && r == nexrSuccess; d++) {
+    a.conns = (const nexr::ResConn*)c->resTable[d];
+    a.status = c->resStatus[d];
+    for (size_t k = 0; k < onDev[d].size(); k++) a.rankOf[k] = onDev[d][k];
+    hipStream_t s = c->streams[onDev[d][0]];
+    if (hipSetDevice(c->resDevs[d]) != hipSuccess ||
+        nexr::launch_resident(kdt, red.op, a, (int)onDev[d].size() * a.nParts * a.team, s) != hipSuccess)
+      r = nexrUnhandledCudaError;
+    else
+      used.push_back(s);
+  }
+  for (size_t d = 0; d < used.size(); d++) {
+    (void)hipSetDevice(c->resDevs[d]);
+    if (hipStreamSynchronize(used[d]) != hipSuccess)
+      r = nexrUnhandledCudaError;
+    else if (__atomic_load_n(c->resStatus[d], __ATOMIC_ACQUIRE) != 0 && r == nexrSuccess)
+      r = nexrInternalError;  // a step wait timed out: the counters are mid-protocol
+  }
+  if (r != nexrSuccess) c->broken = true;
+  return r;
+}
+
 }  // namespace nexr_emu
 
 extern "C" {
+
+NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t c, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t count, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
+  return residentAllReduce(c, sendbuffs, recvbuffs, count, datatype, op);
+}
 
 NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConfig* cfg) {
   DeviceGuard dg(cfg && needsHip(*cfg));
@@ -887,6 +1050,7 @@ NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t c, int rank, int* up, int*
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
   DeviceGuard dg(c && c->needHip);
   if (!c) return nexrInvalidArgument;
+  freeResident(c);
   for (nexrRingComm* ch : c->channels) nexrRingCommDestroy(ch);
   c->channels.clear();
   if (c->peer) {

@@ -20,7 +20,8 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrRingCommDestroy", "nexrPeerRingCommCreate", "nexrPeerRingAllReduce",
                     "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
                     "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
-                    "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv")
+                    "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv",
+                    "nexrRingAllReduceResident")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -62,6 +63,8 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         L.nexrRingAllReduce.restype = ctypes.c_int
+        L.nexrRingAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
+        L.nexrRingAllReduceResident.restype = ctypes.c_int
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         arr = ctypes.POINTER(ctypes.c_void_p)
         for name, extra in (("nexrRingReduceScatter", [i32]), ("nexrRingAllGather", []), ("nexrRingReduce", [i32, i32]),
@@ -137,6 +140,13 @@ class RingComm:
         s = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in sendbuffs])
         r = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in recvbuffs])
         _check(ring_lib().nexrRingAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrRingAllReduce")
+
+    def all_reduce_resident(self, sendbuffs: Sequence[int], recvbuffs: Sequence[int], count: int, datatype: int,
+                            op: int) -> None:
+        """The same all-reduce as one device-resident launch per GPU (nexrRingAllReduceResident)."""
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
+               "nexrRingAllReduceResident")
 
     def _arrays(self, sendbuffs, recvbuffs):
         if len(sendbuffs) != self.n_ranks or len(recvbuffs) != self.n_ranks:

@@ -40,7 +40,8 @@ def test_bench_extra_configs_and_c1():
                                        "c4_i8_max", "c4_i8_prod"}
     for v in d["extra_configs"].values():
         assert 0 < v["frac"] < 1
-    assert all(d["c1_ring"][k]["exact"] for k in ("device", "device_ll", "device_ll128", "host_staged", "cpu_oracle"))
+    assert all(d["c1_ring"][k]["exact"] for k in ("device", "device_resident", "device_ll", "device_ll128", "host_staged",
+                                                       "cpu_oracle"))
 
 
 def test_bench_fanout_rehearsal():

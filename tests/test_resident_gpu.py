@@ -1,0 +1,144 @@
+"""GPU tests of the device-resident ring all-reduce (nexrRingAllReduceResident, nexr_resident.hip):
+every rank's runRing (src/device/all_reduce.h:12-84) inside one launch, its workgroups waiting on
+step counters in HBM. The schedule, chunking and channel split are the host-sequenced ring's, so the
+result must equal, bit for bit, both the fold-order oracle (oracle/ring.py) and nexrRingAllReduce on
+the same communicator."""
+import importlib
+
+import numpy as np
+import pytest
+
+import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+SUM, PROD, MAX, MIN, AVG = 0, 1, 2, 3, 4
+
+
+@pytest.fixture(scope="module")
+def ring(nexr):
+    assert torch.cuda.is_available()
+    return importlib.import_module("nex-nccl_amd.ring")
+
+
+def _dev(arrs):
+    out = [torch.from_numpy(a.copy()).cuda() for a in arrs]
+    torch.cuda.synchronize()
+    return out
+
+
+def _ptrs(ts):
+    return [t.data_ptr() for t in ts]
+
+
+# (ranks, datatype, op, count, buffBytes (0 = 4 MiB), channels)
+CASES = [
+    (2, mg.F32, SUM, 1 << 20, 0, 1),          # C1's shape
+    (3, mg.BF16, SUM, 300_001, 1 << 18, 1),
+    (4, mg.I32, MIN, 70_001, 1 << 16, 2),
+    (3, mg.F16, AVG, 100_003, 1 << 16, 4),
+    (2, mg.I8, MAX, 1_000_003, 0, 2),
+    (5, mg.F64, PROD, 40_000, 1 << 16, 1),
+    (8, mg.F32, AVG, 65_537, 1 << 16, 3),
+    (4, mg.U8, SUM, 17, 1 << 16, 2),
+    (2, mg.I64, AVG, 123_457, 1 << 16, 1),
+    (6, mg.U32, MAX, 999_999, 1 << 17, 2),
+]
+
+
+@pytest.mark.parametrize("n,dt,op,count,buff,nch", CASES)
+def test_resident_matches_oracle_and_host_ring(ring, oracle, n, dt, op, count, buff, nch):
+    from oracle.ring import ring_allreduce_expected
+    inputs = mg.gen_inputs(dt, n, count, 7 * dt + 13 * op + n, special=True)
+    send = _dev(inputs)
+    recv = [torch.zeros_like(s) for s in send]
+    host = [torch.zeros_like(s) for s in send]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000) as comm:
+        comm.all_reduce_resident(_ptrs(send), _ptrs(recv), count, dt, op)
+        comm.all_reduce(_ptrs(send), _ptrs(host), count, dt, op)
+    exp = ring_allreduce_expected(inputs, dt, op, buff or (4 << 20), nch)
+    for r in range(n):
+        got = recv[r].cpu().numpy()
+        assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp[r]), f"rank {r} vs oracle"
+        assert np.array_equal(got.view(np.uint8), host[r].cpu().numpy().view(np.uint8)), f"rank {r} vs host ring"
+
+
+def test_resident_repeated_and_interleaved_with_host_ring(ring, oracle):
+    """Step counters persist in HBM across calls (each member resumes from its own records), and the
+    host-sequenced ring's FIFOs and counters are independent of them: any interleaving stays exact."""
+    from oracle.ring import ring_allreduce_expected
+    n, dt, buff = 3, mg.F32, 1 << 16
+    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=2, timeout_ms=20000) as comm:
+        for it, (count, resident) in enumerate([(50_000, True), (7, True), (200_003, False), (131_072, True),
+                                                (1, True), (99_999, False), (300_000, True)]):
+            inputs = mg.gen_inputs(dt, n, count, 100 + it, special=False)
+            send = _dev(inputs)
+            recv = [torch.zeros_like(s) for s in send]
+            (comm.all_reduce_resident if resident else comm.all_reduce)(_ptrs(send), _ptrs(recv), count, dt, SUM)
+            exp = ring_allreduce_expected(inputs, dt, SUM, buff, 2)
+            for r in range(n):
+                assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), (it, r)
+
+
+def test_resident_in_place(ring, oracle):
+    from oracle.ring import ring_allreduce_expected
+    n, dt, count = 4, mg.BF16, 250_001
+    inputs = mg.gen_inputs(dt, n, count, 5, special=True)
+    buf = _dev(inputs)
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 16, timeout_ms=20000) as comm:
+        comm.all_reduce_resident(_ptrs(buf), _ptrs(buf), count, dt, SUM)
+    exp = ring_allreduce_expected(inputs, dt, SUM, 1 << 16, 1)
+    for r in range(n):
+        assert mg.canon_bytes(dt, buf[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), r
+
+
+def test_resident_misaligned_user_buffers(ring, oracle):
+    """User buffers at odd byte offsets: 16-byte user accesses at any alignment (as the SIMPLE kernel),
+    FIFO pieces stay aligned."""
+    from oracle.ring import ring_allreduce_expected
+    n, dt, count = 2, mg.F16, 77_777
+    inputs = mg.gen_inputs(dt, n, count, 9, special=True)
+    raw_s = [torch.zeros(count * 2 + 64, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    raw_r = [torch.zeros(count * 2 + 64, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    for r in range(n):
+        raw_s[r][3 + r:3 + r + count * 2].copy_(torch.from_numpy(inputs[r].view(np.uint8).copy()).cuda())
+    torch.cuda.synchronize()
+    sp = [raw_s[r].data_ptr() + 3 + r for r in range(n)]
+    rp = [raw_r[r].data_ptr() + 5 + 2 * r for r in range(n)]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 16, n_channels=2, timeout_ms=20000) as comm:
+        comm.all_reduce_resident(sp, rp, count, dt, SUM)
+    exp = ring_allreduce_expected(inputs, dt, SUM, 1 << 16, 2)
+    for r in range(n):
+        got = raw_r[r][5 + 2 * r:5 + 2 * r + count * 2].cpu().numpy().view(np.uint16)
+        assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp[r]), r
+        assert int(raw_r[r][:5 + 2 * r].sum()) == 0 and int(raw_r[r][5 + 2 * r + count * 2:].sum()) == 0, "guard bytes"
+
+
+def test_resident_rejects_what_it_does_not_run(ring):
+    with ring.RingComm(2, ring.DEVICE_MEMORY, 0, protocol=ring.PROTO_LL) as comm:
+        x = torch.zeros(64, device="cuda")
+        with pytest.raises(Exception) as e:
+            comm.all_reduce_resident([x.data_ptr()] * 2, [x.data_ptr()] * 2, 64, mg.F32, SUM)
+        assert "InvalidUsage" in str(e.value) or "5" in str(e.value)
+
+
+def test_resident_across_gpus(ring, oracle):
+    """Ranks on distinct GPUs (rank r on GPU r mod visible): each GPU runs its ranks' part of the
+    schedule in its own launch, FIFO bytes and step counters crossing xGMI. Skipped on one GPU."""
+    from oracle.ring import ring_allreduce_expected
+    nd = torch.cuda.device_count()
+    if nd < 2:
+        pytest.skip("needs 2 GPUs")
+    n, dt, count = min(nd, 8), mg.F32, 1_000_003
+    inputs = mg.gen_inputs(dt, n, count, 77, special=False)
+    send = [torch.from_numpy(x.copy()).to(f"cuda:{r}") for r, x in enumerate(inputs)]
+    recv = [torch.zeros_like(s) for s in send]
+    for r in range(n):
+        torch.cuda.synchronize(r)
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 18, n_channels=2, timeout_ms=20000) as comm:
+        comm.all_reduce_resident(_ptrs(send), _ptrs(recv), count, dt, SUM)
+    exp = ring_allreduce_expected(inputs, dt, SUM, 1 << 18, 2)
+    for r in range(n):
+        assert recv[r].device.index == r
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), r

@@ -168,3 +168,17 @@ def test_ring_with_reference_execution_steps(ring, oracle, n_ranks, dt, op, spec
     exp = ring_allreduce_expected(inputs, dt, op, buff)
     for r in range(n_ranks):
         assert mg.canon_bytes(dt, got[r]) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+def test_resident_all_reduce_needs_device_memory(ring, oracle_fn):
+    """nexrRingAllReduceResident runs only on device-memory SIMPLE communicators: a host-memory one
+    (here with the CPU oracle as its step, so no GPU is touched) is rejected with InvalidUsage before any
+    HIP call, and the communicator stays usable."""
+    x = [np.arange(100, dtype=np.float32) + r for r in range(2)]
+    y = [np.zeros(100, np.float32) for _ in range(2)]
+    with ring.RingComm(2, ring.HOST_MEMORY, 64 << 10, oracle_fn, timeout_ms=20000) as comm:
+        with pytest.raises(ring.NexrError) as e:
+            comm.all_reduce_resident([a.ctypes.data for a in x], [b.ctypes.data for b in y], 100, mg.F32, 0)
+        assert e.value.code == 5  # ncclInvalidUsage
+        comm.all_reduce([a.ctypes.data for a in x], [b.ctypes.data for b in y], 100, mg.F32, 0)
+    assert all(np.array_equal(b, x[0] + x[1]) for b in y)

@@ -86,8 +86,46 @@ def main() -> int:
     out["remote_write"] = {"us": round(t * 1e6, 1), "xgmi_GBps": round(buf / t / 1e9, 1),
                            "alg_GBps": round(3 * buf / t / 1e9, 1), "exact": bool(ok_write)}
     out["ring_processes"] = ring_processes()
+    try:
+        out["resident_ring"] = resident_ring(min(n_dev, 8))
+    except Exception as e:  # noqa: BLE001 - reported, never raised
+        out["resident_ring"] = {"error": repr(e)[:300]}
     print(json.dumps(out), flush=True)
     return 0
+
+
+def resident_ring(n_ranks: int, sizes=(1 << 22, 1 << 26, 1 << 28), channels=(1, 4)):
+    """The ring all-reduce with every step inside one device-resident launch per GPU
+    (nexrRingAllReduceResident): thread ranks of one process, rank r's buffers on GPU r, FIFO bytes and
+    step counters crossing xGMI. fp32 sum of integer-valued inputs, every rank's result checked exactly;
+    algbw = bytes per rank / time, busbw = algbw x 2(n-1)/n (the reference's convention)."""
+    import time
+    import torch
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    nd = torch.cuda.device_count()  # rank r on GPU r (folded onto the visible GPUs when rehearsing)
+    out = {"ranks": n_ranks, "gpus": [r % nd for r in range(n_ranks)]}
+    for nch in channels:
+        for nbytes in sizes:
+            count = nbytes // 4
+            xs = [torch.arange(count, dtype=torch.float32, device=f"cuda:{r % nd}").remainder_(1000) + r
+                  for r in range(n_ranks)]
+            ys = [torch.empty_like(x) for x in xs]
+            for d in range(min(nd, n_ranks)):
+                torch.cuda.synchronize(d)
+            with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=10000) as comm:
+                comm.all_reduce_resident([x.data_ptr() for x in xs], [y.data_ptr() for y in ys], count, 7, 0)
+                iters = 10
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.all_reduce_resident([x.data_ptr() for x in xs], [y.data_ptr() for y in ys], count, 7, 0)
+                dt = (time.perf_counter() - t0) / iters
+            exact = all(torch.equal(y, (torch.arange(count, dtype=torch.float32, device=y.device).remainder_(1000)
+                                        * n_ranks + n_ranks * (n_ranks - 1) // 2)) for y in ys)
+            out[f"ch{nch}_{nbytes}"] = {"ms": round(dt * 1e3, 4), "algbw_GBps": round(nbytes / dt / 1e9, 2),
+                                        "busbw_GBps": round(nbytes * 2 * (n_ranks - 1) / n_ranks / dt / 1e9, 2),
+                                        "exact": bool(exact)}
+            del xs, ys
+    return out
 
 
 PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2}
@@ -163,6 +201,9 @@ def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "104
 
 if __name__ == "__main__":
     a = sys.argv
+    if "--resident-only" in a:  # rehearsal of the resident ring alone: --resident-only N
+        print(json.dumps(resident_ring(int(a[a.index("--resident-only") + 1]))), flush=True)
+        sys.exit(0)
     if "--ring-only" in a:  # rehearsal of the two-rank process ring alone (any number of GPUs)
         print(json.dumps(ring_processes()), flush=True)
         sys.exit(0)
