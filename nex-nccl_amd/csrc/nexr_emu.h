@@ -155,6 +155,7 @@ struct nexrRingComm {
   // block in that device's memory, and a pinned, device-mapped status word.
   std::vector<int> resDevs;
   std::vector<void*> resTable, resCtr;
+  std::vector<void*> resFifo;  // ranks on several GPUs: uncached receive FIFOs [channel * nRanks + rank]
   std::vector<uint32_t*> resStatus;
   // Process ranks: this process is rank `self` only.
   bool peer = false;

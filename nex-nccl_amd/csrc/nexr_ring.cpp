@@ -689,6 +689,12 @@ void freeResident(nexrRingComm* c) {
     if (c->resCtr[i]) (void)hipFree(c->resCtr[i]);
     if (c->resStatus[i]) (void)hipHostFree(c->resStatus[i]);
   }
+  for (size_t k = 0; k < c->resFifo.size(); k++) {
+    if (!c->resFifo[k]) continue;
+    (void)hipSetDevice(c->devices[k % c->cfg.nRanks]);
+    (void)hipFree(c->resFifo[k]);
+  }
+  c->resFifo.clear();
   c->resDevs.clear();
   c->resTable.clear();
   c->resCtr.clear();
@@ -702,7 +708,11 @@ int resDevIndex(const nexrRingComm* c, int rank) {
 }
 
 // First call: per device, a zeroed step-counter block with one record per (channel, rank, team
-// member) for the ranks it hosts, a status word, and the (channel, rank) connection table.
+// member) for the ranks it hosts, a status word, and the (channel, rank) connection table. When the
+// ranks span several GPUs, the step records and the FIFOs are uncached device memory
+// (hipDeviceMallocUncached, as RCCL allocates its P2P FIFOs and flags): their writers then sit on
+// another GPU, whose stores the owner's L2 does not see. On one GPU the communicator's own FIFOs
+// serve, and the records are ordinary device memory.
 nexrResult_t ensureResident(nexrRingComm* c) {
   if (!c->resDevs.empty()) return nexrSuccess;
   const int n = c->cfg.nRanks, nCh = c->cfg.nChannels;
@@ -714,8 +724,16 @@ nexrResult_t ensureResident(nexrRingComm* c) {
   c->resCtr.assign(nd, nullptr);
   c->resStatus.assign(nd, nullptr);
   const size_t ctrBytes = (size_t)nCh * n * nexr::kResMaxTeam * nexr::kResCtrBytes;
+  static const bool forceUncached = [] {  // NEXR_RESIDENT_UNCACHED=1: the multi-GPU layout on one GPU (tests)
+    const char* v = getenv("NEXR_RESIDENT_UNCACHED");
+    return v && v[0] == '1';
+  }();
+  const bool multi = nd > 1 || forceUncached;
+  auto devAlloc = [&](void** p, size_t bytes) {
+    return multi ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) : hipMalloc(p, bytes);
+  };
   for (size_t i = 0; i < nd; i++) {
-    if (hipSetDevice(c->resDevs[i]) != hipSuccess || hipMalloc(&c->resCtr[i], ctrBytes) != hipSuccess ||
+    if (hipSetDevice(c->resDevs[i]) != hipSuccess || devAlloc(&c->resCtr[i], ctrBytes) != hipSuccess ||
         hipMemset(c->resCtr[i], 0, ctrBytes) != hipSuccess ||
         hipHostMalloc((void**)&c->resStatus[i], sizeof(uint32_t), hipHostMallocMapped | hipHostMallocPortable) !=
             hipSuccess ||
@@ -724,16 +742,27 @@ nexrResult_t ensureResident(nexrRingComm* c) {
       return nexrUnhandledCudaError;
     }
   }
+  if (multi) {  // resFifo[ch * n + r]: rank r's receive FIFO of channel ch, on rank r's GPU
+    c->resFifo.assign((size_t)nCh * n, nullptr);
+    for (size_t k = 0; k < c->resFifo.size(); k++) {
+      if (hipSetDevice(c->devices[k % n]) != hipSuccess || devAlloc(&c->resFifo[k], c->cfg.buffBytes) != hipSuccess) {
+        freeResident(c);
+        return nexrUnhandledCudaError;
+      }
+    }
+  }
+  auto fifo = [&](int ch, int r) {
+    return multi ? (char*)c->resFifo[(size_t)ch * n + r] : channelComm(c, ch)->conns[r]->fifo;
+  };
   std::vector<nexr::ResConn> table((size_t)nCh * n);
   for (int ch = 0; ch < nCh; ch++) {
-    nexrRingComm* ck = channelComm(c, ch);
     for (int r = 0; r < n; r++) {
       const int nx = (r + 1) % n;
       auto rec = [&](int rank) {
         return (char*)c->resCtr[resDevIndex(c, rank)] +
                ((size_t)(ch * n + rank) * nexr::kResMaxTeam) * nexr::kResCtrBytes;
       };
-      table[(size_t)ch * n + r] = {ck->conns[r]->fifo, ck->conns[nx]->fifo, rec(r), rec(nx)};
+      table[(size_t)ch * n + r] = {fifo(ch, r), fifo(ch, nx), rec(r), rec(nx)};
     }
   }
   for (size_t i = 0; i < nd; i++) {

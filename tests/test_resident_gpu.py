@@ -142,3 +142,35 @@ def test_resident_across_gpus(ring, oracle):
     for r in range(n):
         assert recv[r].device.index == r
         assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), r
+
+
+def test_resident_uncached_layout_in_a_fresh_process():
+    """NEXR_RESIDENT_UNCACHED=1 gives a one-GPU communicator the layout used when ranks span GPUs
+    (uncached FIFOs and step records, hipDeviceMallocUncached): the C1 shape and a 4-rank, 2-channel
+    bf16 case stay exact. Run in a child process: the switch is read once per process."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import importlib, sys
+sys.path.insert(0, "tests/golden")
+import numpy as np, torch
+import make_golden as mg
+from oracle.ring import ring_allreduce_expected
+ring = importlib.import_module("nex-nccl_amd.ring")
+for n, dt, count, buff, nch in ((2, mg.F32, 1 << 20, 0, 1), (4, mg.BF16, 300_001, 1 << 16, 2)):
+    inputs = mg.gen_inputs(dt, n, count, 3 + n, special=True)
+    send = [torch.from_numpy(a.copy()).cuda() for a in inputs]
+    recv = [torch.zeros_like(s) for s in send]
+    torch.cuda.synchronize()
+    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000) as comm:
+        for _ in range(3):
+            comm.all_reduce_resident([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, dt, 0)
+    exp = ring_allreduce_expected(inputs, dt, 0, buff or (4 << 20), nch)
+    assert all(mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]) for r in range(n)), (n, dt)
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NEXR_RESIDENT_UNCACHED="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
