@@ -102,6 +102,19 @@ NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t comm, const void* const* 
 NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
                                                 void* const* recvbuffs, size_t count, int datatype, int op);
 
+/* The other ring collectives the same way, arguments, results and restrictions as their host-sequenced
+ * forms below and as nexrRingAllReduceResident: runRing of ReduceScatter (reduce_scatter.h:12-52),
+ * AllGather (all_gather.h:12-66, in place when sendbuffs[r] == recvbuffs[r] + r*sendcount elements),
+ * Reduce (reduce.h:12-50) and Broadcast (broadcast.h:12-58) inside one launch per GPU. */
+NEXR_API nexrResult_t nexrRingReduceScatterResident(nexrRingComm_t comm, const void* const* sendbuffs,
+                                                    void* const* recvbuffs, size_t recvcount, int datatype, int op);
+NEXR_API nexrResult_t nexrRingAllGatherResident(nexrRingComm_t comm, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t sendcount, int datatype);
+NEXR_API nexrResult_t nexrRingReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
+                                             void* const* recvbuffs, size_t count, int datatype, int op, int root);
+NEXR_API nexrResult_t nexrRingBroadcastResident(nexrRingComm_t comm, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t count, int datatype, int root);
+
 /* ncclReduceScatter: rank r's sendbuffs[r] holds nRanks*recvcount elements; recvbuffs[r] receives the
  * reduction of every rank's segment r (recvcount elements). */
 NEXR_API nexrResult_t nexrRingReduceScatter(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,

@@ -1,4 +1,4 @@
-// nexr_resident.h — the device-resident ring all-reduce (nexr_resident.hip), shared with its host
+// nexr_resident.h — the device-resident ring collectives (nexr_resident.hip), shared with its host
 // side in nexr_ring.cpp. Not installed; not part of the ABI (include/nexr_ring.h declares the entry
 // point, nexrRingAllReduceResident).
 #pragma once
@@ -24,6 +24,8 @@ struct ResConn {
   char* sendCtr;   // record (ch, r + 1, 0) on the next rank's device
 };
 
+enum { kResAllReduce = 0, kResReduceScatter = 1, kResAllGather = 2, kResReduce = 3, kResBroadcast = 4 };
+
 struct ResParams {
   const ResConn* conns;  // [ch * nRanks + r], in the launching device's memory
   const char* input[kResMaxRanks];
@@ -37,13 +39,35 @@ struct ResParams {
   uint64_t redArg;           // op argument; also the pre-op scalar (Primitives' redOpArgs[0])
   uint32_t* status;          // this device's status word (pinned host memory): 1 = a wait timed out
   uint64_t timeoutTicks;     // s_memrealtime ticks (100 MHz)
-  int stepPerSlice, slicePerChunk;  // StepPerSlice / SlicePerChunk of the ring (collectives.h:17-18)
+  int64_t count;             // ReduceScatter recvcount / AllGather sendcount (rank segment stride)
+  int stepPerSlice, slicePerChunk;  // ProtoSimple<SlicePerChunk, StepPerSlice> (collectives.h:16-25)
+  int coll, root;            // kRes*; root of Reduce / Broadcast
   int nRanks, nParts, team;
 };
 static_assert(sizeof(ResParams) <= 4000, "resident parameters must fit the kernel-argument segment");
 
-// Launches grid = (ranks on this device) * nParts * team workgroups. Returns hipErrorInvalidValue for
-// a datatype/op the kernel does not have.
-hipError_t launch_resident(int dt, int devOp, const ResParams& p, int grid, hipStream_t s);
+// Launches grid = (ranks on this device) * nParts * team workgroups; one entry point per datatype,
+// defined in the object compiled with -DNEXR_DT=<dt>. hipErrorInvalidValue for an op the datatype
+// does not have.
+#define NEXR_DECLARE_RESIDENT(dt) hipError_t launch_resident_dt##dt(int devOp, const ResParams& p, int grid, hipStream_t s);
+NEXR_DECLARE_RESIDENT(0) NEXR_DECLARE_RESIDENT(1) NEXR_DECLARE_RESIDENT(2) NEXR_DECLARE_RESIDENT(3)
+NEXR_DECLARE_RESIDENT(4) NEXR_DECLARE_RESIDENT(5) NEXR_DECLARE_RESIDENT(6) NEXR_DECLARE_RESIDENT(7)
+NEXR_DECLARE_RESIDENT(8) NEXR_DECLARE_RESIDENT(9)
+#undef NEXR_DECLARE_RESIDENT
+inline hipError_t launch_resident(int dt, int devOp, const ResParams& p, int grid, hipStream_t s) {
+  switch (dt) {
+    case 0: return launch_resident_dt0(devOp, p, grid, s);
+    case 1: return launch_resident_dt1(devOp, p, grid, s);
+    case 2: return launch_resident_dt2(devOp, p, grid, s);
+    case 3: return launch_resident_dt3(devOp, p, grid, s);
+    case 4: return launch_resident_dt4(devOp, p, grid, s);
+    case 5: return launch_resident_dt5(devOp, p, grid, s);
+    case 6: return launch_resident_dt6(devOp, p, grid, s);
+    case 7: return launch_resident_dt7(devOp, p, grid, s);
+    case 8: return launch_resident_dt8(devOp, p, grid, s);
+    case 9: return launch_resident_dt9(devOp, p, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
 
 }  // namespace nexr

@@ -1,7 +1,9 @@
-// nexr_resident.hip — the ring all-reduce as ONE device-resident launch per GPU.
+// nexr_resident.hip — the ring collectives as ONE device-resident launch per GPU.
 //
 // What it runs is the reference's device kernel for ncclAllReduce with NCCL_ALGO_RING /
-// NCCL_PROTO_SIMPLE: runRing (src/device/all_reduce.h:12-84) over Primitives::genericOp
+// NCCL_PROTO_SIMPLE — runRing (src/device/all_reduce.h:12-84), and likewise ReduceScatter
+// (reduce_scatter.h:12-52), AllGather (all_gather.h:12-66), Reduce (reduce.h:12-50) and Broadcast
+// (broadcast.h:12-58) — over Primitives::genericOp
 // (src/device/prims_simple.h:190-330) with the FIFO credit protocol of waitPeer / postPeer
 // (:111-188): NCCL_STEPS = 8 slots of stepBytes per connection, a slice spans StepPerSlice steps, the
 // receiver waits for tail >= step + StepPerSlice, the sender for head + NCCL_STEPS >= step +
@@ -27,8 +29,14 @@
 //   - step counters are 64-bit words, one record per member in its own 128-byte lines, written by
 //     one workgroup and polled by one other; every wait is bounded in time (s_memrealtime) and a
 //     timeout is reported in the device's status word, never a hang.
+// Compiled once per datatype with -DNEXR_DT=<nexrDataType_t value> (see Makefile), like the
+// reduce-copy kernels, so the objects build in parallel.
 #include "nexr_fold.hpp"
 #include "nexr_resident.h"
+
+#ifndef NEXR_DT
+#error "compile with -DNEXR_DT=<datatype>"
+#endif
 
 namespace nexr {
 
@@ -236,9 +244,12 @@ struct ResPrims {
   }
 };
 
-// runRing for ncclAllReduce (all_reduce.h:12-84), one rank's view of one channel part.
+// runRing for ncclAllReduce (all_reduce.h:12-84), one rank's view of one channel part. Primitive
+// shapes op<user src, recv, user dst, send>: sendInput <1,0,0,1>, recvReduceSend <1,1,0,1>,
+// recvReduceCopySend <1,1,1,1>, recvCopySend <0,1,1,1>, recvOutput <0,1,1,0>, recvReduceCopy <1,1,1,0>,
+// copySend <1,0,1,1> (prims_simple.h:897-976).
 template <int D, int OP, bool IsMin>
-__device__ void run_ring(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
+__device__ void run_all_reduce(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks;
   int64_t chunkCount = p.a.chunkCount;
   const int64_t loopCount = nranks * chunkCount;
@@ -270,8 +281,81 @@ __device__ void run_ring(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset
   }
 }
 
+// runRing for ncclReduceScatter (reduce_scatter.h:12-52): a.count is the per-rank recvcount; rank
+// d's segment starts at d * count in every sendbuff.
 template <int D, int OP, bool IsMin>
-__global__ __launch_bounds__(kBlock) void ring_allreduce_resident(ResParams a) {
+__device__ void run_reduce_scatter(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+  const int nranks = p.a.nRanks;
+  const int64_t count = p.a.count, chunkCount = p.a.chunkCount;
+  for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += chunkCount) {
+    const int64_t nelem = imin(chunkCount, partCount - elemOffset);
+    const int64_t dataOffset = partOffset + elemOffset;
+    int rankDest = (r + nranks - 1) % nranks;
+    if (!p.template op<true, false, false, true>(dataOffset + rankDest * count, -1, nelem, false)) return;
+    for (int j = 2; j < nranks; ++j) {
+      rankDest = (r + nranks - j) % nranks;
+      if (!p.template op<true, true, false, true>(dataOffset + rankDest * count, -1, nelem, false)) return;
+    }
+    if (!p.template op<true, true, true, false>(dataOffset + (int64_t)r * count, dataOffset, nelem, true)) return;
+  }
+}
+
+// runRing for ncclAllGather (all_gather.h:12-66): a.count is the per-rank sendcount; in place when
+// the input chunk already sits at its place in the output (:52-56).
+template <int D, int OP, bool IsMin>
+__device__ void run_all_gather(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+  constexpr int esz = ResPrims<D, OP, IsMin>::esz;
+  const int nranks = p.a.nRanks;
+  const int64_t count = p.a.count, chunkCount = p.a.chunkCount;
+  for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += chunkCount) {
+    const int64_t nelem = imin(chunkCount, partCount - elemOffset);
+    const int64_t dataOffset = partOffset + elemOffset;
+    int64_t offset = dataOffset + (int64_t)r * count;
+    const bool inPlace = p.input + dataOffset * esz == p.output + offset * esz;
+    if (!(inPlace ? p.template op<true, false, false, true>(dataOffset, -1, nelem, false)
+                  : p.template op<true, false, true, true>(dataOffset, offset, nelem, false)))
+      return;
+    for (int j = 1; j < nranks - 1; ++j) {
+      offset = dataOffset + (int64_t)((r + nranks - j) % nranks) * count;
+      if (!p.template op<false, true, true, true>(-1, offset, nelem, false)) return;
+    }
+    offset = dataOffset + (int64_t)((r + 1) % nranks) * count;
+    if (!p.template op<false, true, true, false>(-1, offset, nelem, false)) return;
+  }
+}
+
+// runRing for ncclReduce (reduce.h:12-50) and ncclBroadcast (broadcast.h:12-58), ProtoSimple<1,1>.
+template <int D, int OP, bool IsMin>
+__device__ void run_reduce(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+  const int nranks = p.a.nRanks, root = p.a.root, prevRank = (r + nranks - 1) % nranks;
+  for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += p.a.chunkCount) {
+    const int64_t offset = partOffset + elemOffset;
+    const int64_t nelem = imin(p.a.chunkCount, partCount - elemOffset);
+    bool ok;
+    if (prevRank == root) ok = p.template op<true, false, false, true>(offset, -1, nelem, false);
+    else if (r == root) ok = p.template op<true, true, true, false>(offset, offset, nelem, true);
+    else ok = p.template op<true, true, false, true>(offset, -1, nelem, false);
+    if (!ok) return;
+  }
+}
+template <int D, int OP, bool IsMin>
+__device__ void run_broadcast(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+  const int nranks = p.a.nRanks, root = p.a.root, nextRank = (r + 1) % nranks;
+  for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += p.a.chunkCount) {
+    const int64_t offset = partOffset + elemOffset;
+    const int64_t nelem = imin(p.a.chunkCount, partCount - elemOffset);
+    bool ok;
+    if (r == root)
+      ok = p.input == p.output ? p.template op<true, false, false, true>(offset, -1, nelem, false)
+                               : p.template op<true, false, true, true>(offset, offset, nelem, false);
+    else if (nextRank == root) ok = p.template op<false, true, true, false>(-1, offset, nelem, false);
+    else ok = p.template op<false, true, true, true>(-1, offset, nelem, false);
+    if (!ok) return;
+  }
+}
+
+template <int D, int OP, bool IsMin>
+__global__ __launch_bounds__(kBlock) void ring_resident(ResParams a) {
   __shared__ ResShared sh;
   const int member = blockIdx.x % a.team;
   const int part = (blockIdx.x / a.team) % a.nParts;
@@ -289,21 +373,31 @@ __global__ __launch_bounds__(kBlock) void ring_allreduce_resident(ResParams a) {
   p.member = member;
   p.sh = &sh;
   p.attach();
-  run_ring(p, rank, a.partOffset[part], a.partCount[part]);
+  const int64_t off = a.partOffset[part], cnt = a.partCount[part];
+  switch (a.coll) {
+    case kResAllReduce: run_all_reduce(p, rank, off, cnt); break;
+    case kResReduceScatter: run_reduce_scatter(p, rank, off, cnt); break;
+    case kResAllGather: run_all_gather(p, rank, off, cnt); break;
+    case kResReduce: run_reduce(p, rank, off, cnt); break;
+    case kResBroadcast: run_broadcast(p, rank, off, cnt); break;
+  }
 }
 
 template <int D, int OP>
 static hipError_t launch_op(const ResParams& p, int grid, hipStream_t s) {
-  const void* fn = (const void*)&ring_allreduce_resident<D, OP, false>;
+  const void* fn = (const void*)&ring_resident<D, OP, false>;
   if constexpr (OP == nexrDevMinMax) {
-    if ((p.redArg & 1) == 0) fn = (const void*)&ring_allreduce_resident<D, OP, true>;  // isMin, reduce_kernel.h:64
+    if ((p.redArg & 1) == 0) fn = (const void*)&ring_resident<D, OP, true>;  // isMin, reduce_kernel.h:64
   }
   void* args[] = {const_cast<ResParams*>(&p)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
 }
 
-template <int D>
-static hipError_t launch_dt(int op, const ResParams& p, int grid, hipStream_t s) {
+#define NEXR_CAT2(a, b) a##b
+#define NEXR_CAT(a, b) NEXR_CAT2(a, b)
+
+hipError_t NEXR_CAT(launch_resident_dt, NEXR_DT)(int op, const ResParams& p, int grid, hipStream_t s) {
+  constexpr int D = NEXR_DT;
   switch (op) {
     case nexrDevSum: return launch_op<D, nexrDevSum>(p, grid, s);
     case nexrDevProd: return launch_op<D, nexrDevProd>(p, grid, s);
@@ -312,22 +406,6 @@ static hipError_t launch_dt(int op, const ResParams& p, int grid, hipStream_t s)
     case nexrDevSumPostDiv:
       if constexpr (Ty<D>::kIsInt) return launch_op<D, nexrDevSumPostDiv>(p, grid, s);
       break;
-  }
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_resident(int dt, int op, const ResParams& p, int grid, hipStream_t s) {
-  switch (dt) {
-    case nexrInt8: return launch_dt<nexrInt8>(op, p, grid, s);
-    case nexrUint8: return launch_dt<nexrUint8>(op, p, grid, s);
-    case nexrInt32: return launch_dt<nexrInt32>(op, p, grid, s);
-    case nexrUint32: return launch_dt<nexrUint32>(op, p, grid, s);
-    case nexrInt64: return launch_dt<nexrInt64>(op, p, grid, s);
-    case nexrUint64: return launch_dt<nexrUint64>(op, p, grid, s);
-    case nexrFloat16: return launch_dt<nexrFloat16>(op, p, grid, s);
-    case nexrFloat32: return launch_dt<nexrFloat32>(op, p, grid, s);
-    case nexrFloat64: return launch_dt<nexrFloat64>(op, p, grid, s);
-    case nexrBfloat16: return launch_dt<nexrBfloat16>(op, p, grid, s);
   }
   return hipErrorInvalidValue;
 }

@@ -791,8 +791,8 @@ int residentTeam(int ranksOnDevice, int nParts, size_t sliceBytes) {
   return (int)std::max(1l, std::min<long>(t, nexr::kResMaxTeam));
 }
 
-nexrResult_t residentAllReduce(nexrRingComm* c, const void* const* sendbuffs, void* const* recvbuffs, size_t count,
-                               int datatype, int op) {
+nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* const* sendbuffs, void* const* recvbuffs,
+                                size_t count, int datatype, int op, int root) {
   if (!c || c->peer) return nexrInvalidArgument;
   if (c->cfg.memMode != nexrRingDeviceMemory || c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
   int sem = nexrSemanticsNccl;
@@ -802,9 +802,13 @@ nexrResult_t residentAllReduce(nexrRingComm* c, const void* const* sendbuffs, vo
   nexrResult_t r = prepare(c, datatype, op, &esz, &red);
   if (r != nexrSuccess) return r;
   const int n = c->cfg.nRanks;
+  if ((coll == kReduce || coll == kBroadcast) && (root < 0 || root >= n)) return nexrInvalidArgument;
   if (!sendbuffs || !recvbuffs) return nexrInvalidArgument;
-  for (int i = 0; i < n; i++)
-    if (!sendbuffs[i] || !recvbuffs[i]) return nexrInvalidArgument;
+  for (int i = 0; i < n; i++) {  // as ringCollective: Broadcast needs only the root's send buffer,
+    const bool needSend = coll != kBroadcast || i == root;  // Reduce only the root's recv buffer
+    const bool needRecv = coll != kReduce || i == root;
+    if ((needSend && !sendbuffs[i]) || (needRecv && !recvbuffs[i])) return nexrInvalidArgument;
+  }
   if (count == 0) return nexrSuccess;
   if (n == 1) return oneRank(c, 0, sendbuffs[0], recvbuffs[0], count, datatype, red, esz);
   if (n > nexr::kResMaxRanks) return nexrInvalidUsage;
@@ -814,9 +818,17 @@ nexrResult_t residentAllReduce(nexrRingComm* c, const void* const* sendbuffs, vo
     kdt = datatype == nexrInt8 ? nexrUint8 : datatype == nexrInt32 ? nexrUint32 : datatype == nexrInt64 ? nexrUint64 : datatype;
   r = ensureResident(c);
   if (r != nexrSuccess) return r;
-  const Geom g = kGeomRing;
-  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, /*ncclFuncAllReduce*/ 2);
+  const Geom g = (coll == kReduce || coll == kBroadcast) ? kGeomPipe : kGeomRing;
+  const int trafficPerByte = coll == kAllReduce ? 2 : (coll == kReduceScatter || coll == kAllGather) ? n : 1;
+  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, trafficPerByte);
   nexr::ResParams a{};
+  a.coll = coll == kAllReduce       ? nexr::kResAllReduce
+           : coll == kReduceScatter ? nexr::kResReduceScatter
+           : coll == kAllGather     ? nexr::kResAllGather
+           : coll == kReduce        ? nexr::kResReduce
+                                    : nexr::kResBroadcast;
+  a.root = root;
+  a.count = (int64_t)count;
   a.nRanks = n;
   a.nParts = (int)parts.size();
   for (size_t i = 0; i < parts.size(); i++) {
@@ -873,7 +885,31 @@ extern "C" {
 NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t c, const void* const* sendbuffs,
                                                 void* const* recvbuffs, size_t count, int datatype, int op) {
   DeviceGuard dg(c && c->needHip);
-  return residentAllReduce(c, sendbuffs, recvbuffs, count, datatype, op);
+  return residentCollective(c, kAllReduce, sendbuffs, recvbuffs, count, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrRingReduceScatterResident(nexrRingComm_t c, const void* const* sendbuffs,
+                                                    void* const* recvbuffs, size_t recvcount, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
+  return residentCollective(c, kReduceScatter, sendbuffs, recvbuffs, recvcount, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrRingAllGatherResident(nexrRingComm_t c, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t sendcount, int datatype) {
+  DeviceGuard dg(c && c->needHip);
+  return residentCollective(c, kAllGather, sendbuffs, recvbuffs, sendcount, datatype, nexrSum, 0);
+}
+
+NEXR_API nexrResult_t nexrRingReduceResident(nexrRingComm_t c, const void* const* sendbuffs, void* const* recvbuffs,
+                                             size_t count, int datatype, int op, int root) {
+  DeviceGuard dg(c && c->needHip);
+  return residentCollective(c, kReduce, sendbuffs, recvbuffs, count, datatype, op, root);
+}
+
+NEXR_API nexrResult_t nexrRingBroadcastResident(nexrRingComm_t c, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t count, int datatype, int root) {
+  DeviceGuard dg(c && c->needHip);
+  return residentCollective(c, kBroadcast, sendbuffs, recvbuffs, count, datatype, nexrSum, root);
 }
 
 NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConfig* cfg) {

@@ -21,7 +21,8 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
                     "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
                     "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv",
-                    "nexrRingAllReduceResident")
+                    "nexrRingAllReduceResident", "nexrRingReduceScatterResident", "nexrRingAllGatherResident",
+                    "nexrRingReduceResident", "nexrRingBroadcastResident")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -65,6 +66,11 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingAllReduce.restype = ctypes.c_int
         L.nexrRingAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
         L.nexrRingAllReduceResident.restype = ctypes.c_int
+        _arr, _i, _sz = ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t
+        for f, extra in ((L.nexrRingReduceScatterResident, [_i, _i]), (L.nexrRingAllGatherResident, [_i]),
+                         (L.nexrRingReduceResident, [_i, _i, _i]), (L.nexrRingBroadcastResident, [_i, _i])):
+            f.argtypes = [ctypes.c_void_p, _arr, _arr, _sz] + extra
+            f.restype = ctypes.c_int
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         arr = ctypes.POINTER(ctypes.c_void_p)
         for name, extra in (("nexrRingReduceScatter", [i32]), ("nexrRingAllGather", []), ("nexrRingReduce", [i32, i32]),
@@ -147,6 +153,26 @@ class RingComm:
         s, r = self._arrays(sendbuffs, recvbuffs)
         _check(ring_lib().nexrRingAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
                "nexrRingAllReduceResident")
+
+    def reduce_scatter_resident(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingReduceScatterResident(self._h, s, r, int(recvcount), int(datatype), int(op)),
+               "nexrRingReduceScatterResident")
+
+    def all_gather_resident(self, sendbuffs, recvbuffs, sendcount: int, datatype: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingAllGatherResident(self._h, s, r, int(sendcount), int(datatype)),
+               "nexrRingAllGatherResident")
+
+    def reduce_resident(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int, root: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingReduceResident(self._h, s, r, int(count), int(datatype), int(op), int(root)),
+               "nexrRingReduceResident")
+
+    def broadcast_resident(self, sendbuffs, recvbuffs, count: int, datatype: int, root: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrRingBroadcastResident(self._h, s, r, int(count), int(datatype), int(root)),
+               "nexrRingBroadcastResident")
 
     def _arrays(self, sendbuffs, recvbuffs):
         if len(sendbuffs) != self.n_ranks or len(recvbuffs) != self.n_ranks:

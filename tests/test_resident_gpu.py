@@ -174,3 +174,71 @@ print("ok")
     env = dict(os.environ, NEXR_RESIDENT_UNCACHED="1")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def _ptrs0(ts):
+    return [t.data_ptr() if t is not None else 0 for t in ts]
+
+
+@pytest.mark.parametrize("n,dt,op,nch", [(2, mg.F32, SUM, 1), (3, mg.BF16, AVG, 2), (4, mg.I32, MIN, 4),
+                                         (5, mg.F16, PROD, 1), (8, mg.U8, MAX, 2)])
+def test_resident_reduce_scatter(ring, oracle, n, dt, op, nch):
+    from oracle.ring import reduce_scatter_expected
+    count = 70_001
+    inputs = mg.gen_inputs(dt, n, count * n, 0x3000 + dt + op, True)
+    send = _dev(inputs)
+    recv = [torch.zeros(count, dtype=s.dtype, device=s.device) for s in send]
+    host = [torch.zeros_like(r) for r in recv]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 16, n_channels=nch, timeout_ms=20000) as comm:
+        comm.reduce_scatter_resident(_ptrs(send), _ptrs(recv), count, dt, op)
+        comm.reduce_scatter(_ptrs(send), _ptrs(host), count, dt, op)
+    exp = reduce_scatter_expected(inputs, dt, op, "simple")
+    for r in range(n):
+        assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+        assert torch.equal(recv[r].view(torch.uint8), host[r].view(torch.uint8)), f"rank {r} vs host ring"
+
+
+@pytest.mark.parametrize("n,nch,in_place", [(2, 1, False), (3, 2, True), (4, 4, False), (8, 1, True)])
+def test_resident_all_gather(ring, oracle, n, nch, in_place):
+    from oracle.ring import all_gather_expected
+    dt, count = mg.F16, 50_003
+    inputs = mg.gen_inputs(dt, n, count, 0x3100 + n, True)
+    recv = _dev([np.zeros(count * n, dtype=inputs[0].dtype) for _ in range(n)])
+    if in_place:
+        for r in range(n):
+            recv[r][r * count:(r + 1) * count].copy_(torch.from_numpy(inputs[r]))
+        send = [recv[r][r * count:] for r in range(n)]
+    else:
+        send = _dev(inputs)
+    torch.cuda.synchronize()
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 16, n_channels=nch, timeout_ms=20000) as comm:
+        comm.all_gather_resident(_ptrs(send), _ptrs(recv), count, dt)
+    exp = all_gather_expected(inputs)
+    for r in range(n):
+        assert recv[r].cpu().numpy().tobytes() == exp[r].tobytes(), f"rank {r}"
+
+
+@pytest.mark.parametrize("n,root,dt,op,nch", [(3, 0, mg.F32, SUM, 1), (4, 2, mg.I8, MAX, 2), (2, 1, mg.BF16, AVG, 4),
+                                              (6, 5, mg.F64, PROD, 2)])
+def test_resident_reduce_and_broadcast(ring, oracle, n, root, dt, op, nch):
+    from oracle.ring import reduce_expected, broadcast_expected
+    count = 90_007
+    inputs = mg.gen_inputs(dt, n, count, 0x3200 + root + dt, True)
+    send = _dev(inputs)
+    red = [torch.zeros_like(send[0]) if r == root else None for r in range(n)]
+    bc = [torch.zeros_like(s) for s in send]
+    bc_in_place = [s.clone() if r == root else torch.zeros_like(s) for r, s in enumerate(send)]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 16, n_channels=nch, timeout_ms=20000) as comm:
+        comm.reduce_resident(_ptrs(send), _ptrs0(red), count, dt, op, root)
+        comm.broadcast_resident([send[r].data_ptr() if r == root else 0 for r in range(n)], _ptrs(bc), count, dt, root)
+        comm.broadcast_resident([bc_in_place[r].data_ptr() if r == root else 0 for r in range(n)], _ptrs(bc_in_place),
+                                count, dt, root)
+        comm.all_reduce_resident(_ptrs(send), _ptrs(bc_in_place), count, dt, op)  # after Broadcast's 1-step slices
+    assert mg.canon_bytes(dt, red[root].cpu().numpy()) == mg.canon_bytes(dt, reduce_expected(inputs, dt, op, root,
+                                                                                            "simple"))
+    for r, e in enumerate(broadcast_expected(inputs, root)):
+        assert bc[r].cpu().numpy().tobytes() == e.tobytes(), f"rank {r}"
+    from oracle.ring import ring_allreduce_expected
+    exp = ring_allreduce_expected(inputs, dt, op, 1 << 16, nch)
+    for r in range(n):
+        assert mg.canon_bytes(dt, bc_in_place[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"all-reduce rank {r}"
