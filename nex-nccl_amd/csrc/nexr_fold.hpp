@@ -27,6 +27,18 @@ struct Fold {
       for (int s = 0; s < K; s++) factor[s] = T::splat(p.pre[s]);
     }
   }
+  // One pre-op scalar for source 0 only (a Primitives' redOpArgs[0] with PreOpSrcs <= 1), without an
+  // RCParams in memory: the resident ring's form.
+  __device__ Fold(uint64_t pre0, int nPre, bool postOp, uint64_t arg) {
+    nPreOp = nPre;
+    post = (OP == nexrDevSumPostDiv) && postOp;
+    redArg = arg;
+    canon = (K >= 2) || (OP == nexrDevPreMulSum && nPre > 0);
+    if constexpr (OP == nexrDevPreMulSum) {
+#pragma unroll
+      for (int s = 0; s < K; s++) factor[s] = T::splat(pre0);
+    }
+  }
   __device__ __forceinline__ V pre(V x, int s) const {
     if constexpr (OP == nexrDevPreMulSum) {
       if (s < nPreOp) return T::mul(x, factor[s]);  // Apply_PreOp<FuncPreMulSum> :498-518

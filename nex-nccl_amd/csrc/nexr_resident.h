@@ -49,7 +49,9 @@ static_assert(sizeof(ResParams) <= 4000, "resident parameters must fit the kerne
 // Launches grid = (ranks on this device) * nParts * team workgroups; one entry point per datatype,
 // defined in the object compiled with -DNEXR_DT=<dt>. hipErrorInvalidValue for an op the datatype
 // does not have.
-#define NEXR_DECLARE_RESIDENT(dt) hipError_t launch_resident_dt##dt(int devOp, const ResParams& p, int grid, hipStream_t s);
+#define NEXR_DECLARE_RESIDENT(dt)                                                                \
+  hipError_t launch_resident_dt##dt(int devOp, const ResParams& p, int grid, hipStream_t s); \
+  hipError_t resident_blocks_per_cu_dt##dt(int devOp, uint64_t redArg, int* blocks);
 NEXR_DECLARE_RESIDENT(0) NEXR_DECLARE_RESIDENT(1) NEXR_DECLARE_RESIDENT(2) NEXR_DECLARE_RESIDENT(3)
 NEXR_DECLARE_RESIDENT(4) NEXR_DECLARE_RESIDENT(5) NEXR_DECLARE_RESIDENT(6) NEXR_DECLARE_RESIDENT(7)
 NEXR_DECLARE_RESIDENT(8) NEXR_DECLARE_RESIDENT(9)
@@ -66,6 +68,23 @@ inline hipError_t launch_resident(int dt, int devOp, const ResParams& p, int gri
     case 7: return launch_resident_dt7(devOp, p, grid, s);
     case 8: return launch_resident_dt8(devOp, p, grid, s);
     case 9: return launch_resident_dt9(devOp, p, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+// Workgroups of the (datatype, op) kernel one CU holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor):
+// a device's grid must fit in this times its CUs, since a rank's workgroups wait on each other.
+inline hipError_t resident_blocks_per_cu(int dt, int devOp, uint64_t redArg, int* blocks) {
+  switch (dt) {
+    case 0: return resident_blocks_per_cu_dt0(devOp, redArg, blocks);
+    case 1: return resident_blocks_per_cu_dt1(devOp, redArg, blocks);
+    case 2: return resident_blocks_per_cu_dt2(devOp, redArg, blocks);
+    case 3: return resident_blocks_per_cu_dt3(devOp, redArg, blocks);
+    case 4: return resident_blocks_per_cu_dt4(devOp, redArg, blocks);
+    case 5: return resident_blocks_per_cu_dt5(devOp, redArg, blocks);
+    case 6: return resident_blocks_per_cu_dt6(devOp, redArg, blocks);
+    case 7: return resident_blocks_per_cu_dt7(devOp, redArg, blocks);
+    case 8: return resident_blocks_per_cu_dt8(devOp, redArg, blocks);
+    case 9: return resident_blocks_per_cu_dt9(devOp, redArg, blocks);
   }
   return hipErrorInvalidValue;
 }

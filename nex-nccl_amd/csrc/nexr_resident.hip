@@ -67,6 +67,14 @@ __device__ __forceinline__ int64_t imin(int64_t x, int64_t y) { return x < y ? x
 __device__ __forceinline__ int64_t imax(int64_t x, int64_t y) { return x > y ? x : y; }
 __device__ __forceinline__ int64_t divUp64(int64_t x, int64_t y) { return (x + y - 1) / y; }
 
+// The call-wide scalars every workgroup needs, copied out of the kernel argument.
+struct ResScalars {
+  int64_t chunkCount, stepElems, count;
+  uint64_t stepBytes, redArg, timeoutTicks;
+  uint32_t* status;
+  int stepPerSlice, slicePerChunk, team, nRanks, root;
+};
+
 struct ResShared {
   uint64_t recvStep, sendStep;
   int ok;
@@ -136,7 +144,7 @@ __device__ __forceinline__ void piece(const char* usrc, const char* rfifo, char*
 template <int D, int OP, bool IsMin>
 struct ResPrims {
   static constexpr int esz = 16 / Ty<D>::EPP;
-  const ResParams& a;
+  ResScalars a;  // by value: a reference to the kernel argument would copy it to scratch
   const char* input;
   char* output;
   char* recvFifo;
@@ -152,7 +160,7 @@ struct ResPrims {
   // waitPeer's spin (prims_simple.h:116-123), thread 0 only, bounded like checkAbort
   // (primitives.h:142-156): false after a timeout (status set) or once another workgroup's timeout
   // is visible in the status word.
-  __device__ bool wait_ge(const char* p, uint64_t target) const {
+  __device__ __forceinline__ bool wait_ge(const char* p, uint64_t target) const {
     uint64_t t0 = 0;
     for (uint32_t spins = 0;; spins++) {
       if (ctr_ld(p) >= target) return true;
@@ -170,7 +178,7 @@ struct ResPrims {
 
   // loadRecvConn / loadSendConn (prims_simple.h:512-517, :557-558): steps resume from the previous
   // collective's, rounded up to SlicePerChunk * StepPerSlice, the receiver publishing its rounded step.
-  __device__ void attach() {
+  __device__ __forceinline__ void attach() {
     if (threadIdx.x == 0) {
       const uint64_t cs = (uint64_t)(a.stepPerSlice * a.slicePerChunk);
       const uint64_t rs = (ctr_ld(recvHead) + cs - 1) / cs * cs;
@@ -187,14 +195,10 @@ struct ResPrims {
 
   // genericOp<0, 0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330) for this member's pieces.
   template <bool US, bool R, bool UD, bool S>
-  __device__ bool op(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
+  __device__ __forceinline__ bool op(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
     constexpr int K = (int)US + (int)R;
-    RCParams p{};
-    p.pre[0] = a.redArg;
-    p.redArg = a.redArg;
-    p.nPreOp = US ? 1 : 0;  // PreOpSrcs = SrcBuf == Input (prims_simple.h:279-280)
-    p.postOp = postOp ? 1 : 0;
-    const Fold<D, OP, K, IsMin> f(p);
+    // PreOpSrcs = SrcBuf == Input (prims_simple.h:279-280), preOpArgs = redOpArgs
+    const Fold<D, OP, K, IsMin> f(a.redArg, US ? 1 : 0, postOp, a.redArg);
     nelem = nelem < 0 ? 0 : nelem;
     int64_t sliceSize = a.stepElems * a.stepPerSlice;
     sliceSize = imax(divUp64(nelem, 16 * (int64_t)a.slicePerChunk) * 16, sliceSize / 32);
@@ -249,7 +253,7 @@ struct ResPrims {
 // recvReduceCopySend <1,1,1,1>, recvCopySend <0,1,1,1>, recvOutput <0,1,1,0>, recvReduceCopy <1,1,1,0>,
 // copySend <1,0,1,1> (prims_simple.h:897-976).
 template <int D, int OP, bool IsMin>
-__device__ void run_all_reduce(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_all_reduce(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks;
   int64_t chunkCount = p.a.chunkCount;
   const int64_t loopCount = nranks * chunkCount;
@@ -284,7 +288,7 @@ __device__ void run_all_reduce(ResPrims<D, OP, IsMin>& p, int rank, int64_t part
 // runRing for ncclReduceScatter (reduce_scatter.h:12-52): a.count is the per-rank recvcount; rank
 // d's segment starts at d * count in every sendbuff.
 template <int D, int OP, bool IsMin>
-__device__ void run_reduce_scatter(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_reduce_scatter(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks;
   const int64_t count = p.a.count, chunkCount = p.a.chunkCount;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += chunkCount) {
@@ -303,7 +307,7 @@ __device__ void run_reduce_scatter(ResPrims<D, OP, IsMin>& p, int r, int64_t par
 // runRing for ncclAllGather (all_gather.h:12-66): a.count is the per-rank sendcount; in place when
 // the input chunk already sits at its place in the output (:52-56).
 template <int D, int OP, bool IsMin>
-__device__ void run_all_gather(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_all_gather(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   constexpr int esz = ResPrims<D, OP, IsMin>::esz;
   const int nranks = p.a.nRanks;
   const int64_t count = p.a.count, chunkCount = p.a.chunkCount;
@@ -326,7 +330,7 @@ __device__ void run_all_gather(ResPrims<D, OP, IsMin>& p, int r, int64_t partOff
 
 // runRing for ncclReduce (reduce.h:12-50) and ncclBroadcast (broadcast.h:12-58), ProtoSimple<1,1>.
 template <int D, int OP, bool IsMin>
-__device__ void run_reduce(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_reduce(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks, root = p.a.root, prevRank = (r + nranks - 1) % nranks;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += p.a.chunkCount) {
     const int64_t offset = partOffset + elemOffset;
@@ -339,7 +343,7 @@ __device__ void run_reduce(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset,
   }
 }
 template <int D, int OP, bool IsMin>
-__device__ void run_broadcast(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_broadcast(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks, root = p.a.root, nextRank = (r + 1) % nranks;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += p.a.chunkCount) {
     const int64_t offset = partOffset + elemOffset;
@@ -361,7 +365,8 @@ __global__ __launch_bounds__(kBlock) void ring_resident(ResParams a) {
   const int part = (blockIdx.x / a.team) % a.nParts;
   const int rank = a.rankOf[blockIdx.x / (a.team * a.nParts)];
   const ResConn& c = a.conns[a.partChannel[part] * a.nRanks + rank];
-  ResPrims<D, OP, IsMin> p{a};
+  ResPrims<D, OP, IsMin> p{{a.chunkCount, a.stepElems, a.count, a.stepBytes, a.redArg, a.timeoutTicks, a.status,
+                            a.stepPerSlice, a.slicePerChunk, a.team, a.nRanks, a.root}};
   p.input = a.input[rank];
   p.output = a.output[rank];
   p.recvFifo = c.recvFifo;
@@ -384,30 +389,41 @@ __global__ __launch_bounds__(kBlock) void ring_resident(ResParams a) {
 }
 
 template <int D, int OP>
-static hipError_t launch_op(const ResParams& p, int grid, hipStream_t s) {
-  const void* fn = (const void*)&ring_resident<D, OP, false>;
+static const void* kernel_op(uint64_t redArg) {
   if constexpr (OP == nexrDevMinMax) {
-    if ((p.redArg & 1) == 0) fn = (const void*)&ring_resident<D, OP, true>;  // isMin, reduce_kernel.h:64
+    if ((redArg & 1) == 0) return (const void*)&ring_resident<D, OP, true>;  // isMin, reduce_kernel.h:64
   }
-  void* args[] = {const_cast<ResParams*>(&p)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+  return (const void*)&ring_resident<D, OP, false>;
+}
+
+template <int D>
+static const void* kernel_for(int op, uint64_t redArg) {
+  switch (op) {
+    case nexrDevSum: return kernel_op<D, nexrDevSum>(redArg);
+    case nexrDevProd: return kernel_op<D, nexrDevProd>(redArg);
+    case nexrDevMinMax: return kernel_op<D, nexrDevMinMax>(redArg);
+    case nexrDevPreMulSum: return kernel_op<D, nexrDevPreMulSum>(redArg);
+    case nexrDevSumPostDiv:
+      if constexpr (Ty<D>::kIsInt) return kernel_op<D, nexrDevSumPostDiv>(redArg);
+      break;
+  }
+  return nullptr;
 }
 
 #define NEXR_CAT2(a, b) a##b
 #define NEXR_CAT(a, b) NEXR_CAT2(a, b)
 
 hipError_t NEXR_CAT(launch_resident_dt, NEXR_DT)(int op, const ResParams& p, int grid, hipStream_t s) {
-  constexpr int D = NEXR_DT;
-  switch (op) {
-    case nexrDevSum: return launch_op<D, nexrDevSum>(p, grid, s);
-    case nexrDevProd: return launch_op<D, nexrDevProd>(p, grid, s);
-    case nexrDevMinMax: return launch_op<D, nexrDevMinMax>(p, grid, s);
-    case nexrDevPreMulSum: return launch_op<D, nexrDevPreMulSum>(p, grid, s);
-    case nexrDevSumPostDiv:
-      if constexpr (Ty<D>::kIsInt) return launch_op<D, nexrDevSumPostDiv>(p, grid, s);
-      break;
-  }
-  return hipErrorInvalidValue;
+  const void* fn = kernel_for<NEXR_DT>(op, p.redArg);
+  if (!fn) return hipErrorInvalidValue;
+  void* args[] = {const_cast<ResParams*>(&p)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+}
+
+hipError_t NEXR_CAT(resident_blocks_per_cu_dt, NEXR_DT)(int op, uint64_t redArg, int* blocks) {
+  const void* fn = kernel_for<NEXR_DT>(op, redArg);
+  if (!fn) return hipErrorInvalidValue;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fn, kBlock, 0);
 }
 
 }  // namespace nexr

@@ -852,9 +852,19 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
   for (int i = 0; i < n; i++) onDev[resDevIndex(c, i)].push_back(i);
   for (const auto& v : onDev) busiest = std::max(busiest, (int)v.size());
   a.team = residentTeam(busiest, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
-  // Every workgroup of a device's grid must be resident at once (a rank's blocks wait on others):
-  // at most four 256-lane workgroups per CU.
-  if ((long)busiest * a.nParts * a.team > 1024) return nexrInvalidUsage;
+  // Every workgroup of a device's grid must be resident at once (a rank's workgroups wait on others'):
+  // the team shrinks to what the kernel's occupancy allows on every device used.
+  long capacity = -1;
+  for (size_t d = 0; d < c->resDevs.size(); d++) {
+    int perCU = 0, cus = 0;
+    if (hipSetDevice(c->resDevs[d]) != hipSuccess || nexr::resident_blocks_per_cu(kdt, red.op, red.scalarArg, &perCU) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->resDevs[d]) != hipSuccess)
+      return nexrUnhandledCudaError;
+    const long cap = (long)perCU * cus;
+    capacity = capacity < 0 ? cap : std::min(capacity, cap);
+  }
+  if ((long)busiest * a.nParts * a.team > capacity) a.team = (int)(capacity / ((long)busiest * a.nParts));
+  if (a.team < 1) return nexrInvalidUsage;
   std::vector<hipStream_t> used;
   for (size_t d = 0; d < onDev.size() && r == nexrSuccess; d++) {
     a.conns = (const nexr::ResConn*)c->resTable[d];

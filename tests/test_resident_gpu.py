@@ -242,3 +242,35 @@ def test_resident_reduce_and_broadcast(ring, oracle, n, root, dt, op, nch):
     exp = ring_allreduce_expected(inputs, dt, op, 1 << 16, nch)
     for r in range(n):
         assert mg.canon_bytes(dt, bc_in_place[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"all-reduce rank {r}"
+
+
+def test_resident_team_shrinks_to_kernel_occupancy():
+    """NEXR_RESIDENT_TEAM=128 with 8 ranks x 2 channels asks for 2,048 workgroups of the int8 kernel
+    on one GPU, more than its occupancy lets be resident at once: the team shrinks to fit
+    (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs) instead of waiting on workgroups that cannot
+    start, and the result stays exact. Child process: the switch is read once per process."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import importlib, sys
+sys.path.insert(0, "tests/golden")
+import torch
+import make_golden as mg
+from oracle.ring import ring_allreduce_expected
+ring = importlib.import_module("nex-nccl_amd.ring")
+n, dt, count, buff, nch = 8, mg.I8, 1_000_003, 1 << 18, 2
+inputs = mg.gen_inputs(dt, n, count, 41, special=True)
+send = [torch.from_numpy(a.copy()).cuda() for a in inputs]
+recv = [torch.zeros_like(s) for s in send]
+torch.cuda.synchronize()
+with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000) as comm:
+    comm.all_reduce_resident([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, dt, 2)
+exp = ring_allreduce_expected(inputs, dt, 2, buff, nch)
+assert all(mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]) for r in range(n))
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NEXR_RESIDENT_TEAM="128")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
