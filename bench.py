@@ -16,7 +16,8 @@ Either N > 1 way also times an N=1 leg on GPU 0 in the same run, and every GPU a
 them beside the aggregate under `c5`.
 
 Prints ONE JSON line on rank 0 (keys per the driver contract, plus `roofline`, `cpu_baseline`,
-`h2d_inclusive`, `extra_configs` at N=1 and `per_gpu` / `c5` at N>1).
+`h2d_inclusive`, `extra_configs` / `c1_ring` / `resident_ring` at N=1 and `per_gpu` / `c5` /
+`xgmi_probe` at N>1).
 """
 from __future__ import annotations
 
@@ -337,6 +338,34 @@ def c1_ring(iters: int = 20) -> dict:
     return out
 
 
+def resident_ring(n: int = 2, nbytes: int = 256 << 20, channels: int = 4, iters: int = 10) -> dict:
+    """The ring all-reduce as one device-resident launch (nexrRingAllReduceResident) at a
+    bandwidth size: n emulated ranks on this GPU, fp32 sum of integer-valued inputs (exact check),
+    4 MiB buffers, `channels` channels. bytes_moved_rate counts every byte the schedule reads and
+    writes, S x (6n - 4) per call, FIFO bytes included (they may be Infinity-Cache-served)."""
+    import torch
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    count = nbytes // 4
+    dev = torch.device("cuda", local_device_index())
+    xs = [torch.arange(count, dtype=torch.float32, device=dev).remainder_(1000) + r for r in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    torch.cuda.synchronize(dev)
+    sp, rp = [x.data_ptr() for x in xs], [y.data_ptr() for y in ys]
+    with torch.cuda.device(dev), ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=channels,
+                                               timeout_ms=10000) as comm:
+        comm.all_reduce_resident(sp, rp, count, 7, 0)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            comm.all_reduce_resident(sp, rp, count, 7, 0)
+        dt = (time.perf_counter() - t0) / iters
+    exp = torch.arange(count, dtype=torch.float32, device=dev).remainder_(1000) * n + n * (n - 1) // 2
+    exact = all(torch.equal(y, exp) for y in ys)
+    return {"workload": f"fp32 sum all-reduce, {nbytes >> 20} MiB per rank, {n} emulated ranks on one GPU, ring SIMPLE, "
+                        f"{channels} channels, one device-resident launch per call",
+            "ms_per_call": round(dt * 1e3, 4), "algbw_gbs": round(nbytes / dt / 1e9, 2),
+            "bytes_moved_rate_gbs": round(nbytes * (6 * n - 4) / dt / 1e9, 1), "calls": iters, "exact": bool(exact)}
+
+
 # ---- CPU baseline: the oracle (C restatement) on the benchmarked configuration ------------------
 def usable_cores() -> tuple:
     """(threads to use, how that was decided): the CPUs this process may run on, capped by the
@@ -648,6 +677,7 @@ def main_ranks(args, cfg, pkg) -> dict | None:
                 wl.free()
                 result["extra_configs"] = side_leg(extra_configs, pkg)
                 result["c1_ring"] = side_leg(c1_ring)
+                result["resident_ring"] = side_leg(resident_ring)
             if not args.no_cpu:
                 result["cpu_baseline"] = side_leg(cpu_baseline_entry, cfg, args.cpu_seconds)
             if not args.no_h2d:

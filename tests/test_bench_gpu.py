@@ -42,6 +42,7 @@ def test_bench_extra_configs_and_c1():
         assert 0 < v["frac"] < 1
     assert all(d["c1_ring"][k]["exact"] for k in ("device", "device_resident", "device_ll", "device_ll128", "host_staged",
                                                        "cpu_oracle"))
+    assert d["resident_ring"]["exact"] and d["resident_ring"]["ms_per_call"] > 0
 
 
 def test_bench_fanout_rehearsal():
