@@ -106,6 +106,11 @@ NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t comm, const void*
  * forms below and as nexrRingAllReduceResident: runRing of ReduceScatter (reduce_scatter.h:12-52),
  * AllGather (all_gather.h:12-66, in place when sendbuffs[r] == recvbuffs[r] + r*sendcount elements),
  * Reduce (reduce.h:12-50) and Broadcast (broadcast.h:12-58) inside one launch per GPU. */
+/* The tree ncclAllReduce (runTreeSplit, all_reduce.h:150-230) the same way: per (rank, channel) one team
+ * reduces up and one broadcasts down, as the reference splits a block's threads; same topology,
+ * chunking, results and restrictions as nexrTreeAllReduce / nexrRingAllReduceResident. */
+NEXR_API nexrResult_t nexrTreeAllReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t count, int datatype, int op);
 NEXR_API nexrResult_t nexrRingReduceScatterResident(nexrRingComm_t comm, const void* const* sendbuffs,
                                                     void* const* recvbuffs, size_t recvcount, int datatype, int op);
 NEXR_API nexrResult_t nexrRingAllGatherResident(nexrRingComm_t comm, const void* const* sendbuffs,

@@ -156,6 +156,10 @@ struct nexrRingComm {
   std::vector<int> resDevs;
   std::vector<void*> resTable, resCtr;
   std::vector<void*> resFifo;  // ranks on several GPUs: uncached receive FIFOs [channel * nRanks + rank]
+  // The tree's (nexrTreeAllReduceResident), made by its first call: per device the (channel, rank)
+  // table and the records of connections up[r] (id r) and down[r] (id nRanks + r); on several GPUs
+  // also uncached FIFOs [channel * 2 nRanks + id].
+  std::vector<void*> resTreeTable, resTreeCtr, resTreeFifo;
   std::vector<uint32_t*> resStatus;
   // Process ranks: this process is rank `self` only.
   bool peer = false;

@@ -24,10 +24,28 @@ struct ResConn {
   char* sendCtr;   // record (ch, r + 1, 0) on the next rank's device
 };
 
-enum { kResAllReduce = 0, kResReduceScatter = 1, kResAllGather = 2, kResReduce = 3, kResBroadcast = 4 };
+enum { kResAllReduce = 0, kResReduceScatter = 1, kResAllGather = 2, kResReduce = 3, kResBroadcast = 4,
+       kResTreeAllReduce = 5 };
+
+// One (channel, rank) of the tree all-reduce (runTreeSplit), static for the communicator. Connection
+// up[r] carries r -> parent(r) (its FIFO and records on the parent's GPU), down[r] parent(r) -> r (on
+// r's GPU); the record pointers are member 0's, member g's at + g * kResCtrBytes.
+struct ResTreeConn {
+  char* upRecvFifo[3];  // up[child i]: the children's partial results arrive here
+  char* upRecvCtr[3];
+  char* upSendFifo;     // up[r], on the parent (unused at the root)
+  char* upSendCtr;
+  char* downRecvFifo;   // down[r] (unused at the root)
+  char* downRecvCtr;
+  char* downSendFifo[3];  // down[child i], on the child
+  char* downSendCtr[3];
+  int nDown;            // children, packed first (setTreeDown)
+  int root;
+};
 
 struct ResParams {
   const ResConn* conns;  // [ch * nRanks + r], in the launching device's memory
+  const ResTreeConn* tree;  // [ch * nRanks + r], kResTreeAllReduce only
   const char* input[kResMaxRanks];
   char* output[kResMaxRanks];
   int64_t partOffset[kResMaxParts], partCount[kResMaxParts];
@@ -46,12 +64,12 @@ struct ResParams {
 };
 static_assert(sizeof(ResParams) <= 4000, "resident parameters must fit the kernel-argument segment");
 
-// Launches grid = (ranks on this device) * nParts * team workgroups; one entry point per datatype,
+// Launches grid = (ranks on this device) * nParts * team workgroups (x 2 roles for the tree); one entry point per datatype,
 // defined in the object compiled with -DNEXR_DT=<dt>. hipErrorInvalidValue for an op the datatype
 // does not have.
 #define NEXR_DECLARE_RESIDENT(dt)                                                                \
   hipError_t launch_resident_dt##dt(int devOp, const ResParams& p, int grid, hipStream_t s); \
-  hipError_t resident_blocks_per_cu_dt##dt(int devOp, uint64_t redArg, int* blocks);
+  hipError_t resident_blocks_per_cu_dt##dt(int devOp, uint64_t redArg, int coll, int* blocks);
 NEXR_DECLARE_RESIDENT(0) NEXR_DECLARE_RESIDENT(1) NEXR_DECLARE_RESIDENT(2) NEXR_DECLARE_RESIDENT(3)
 NEXR_DECLARE_RESIDENT(4) NEXR_DECLARE_RESIDENT(5) NEXR_DECLARE_RESIDENT(6) NEXR_DECLARE_RESIDENT(7)
 NEXR_DECLARE_RESIDENT(8) NEXR_DECLARE_RESIDENT(9)
@@ -73,18 +91,18 @@ inline hipError_t launch_resident(int dt, int devOp, const ResParams& p, int gri
 }
 // Workgroups of the (datatype, op) kernel one CU holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor):
 // a device's grid must fit in this times its CUs, since a rank's workgroups wait on each other.
-inline hipError_t resident_blocks_per_cu(int dt, int devOp, uint64_t redArg, int* blocks) {
+inline hipError_t resident_blocks_per_cu(int dt, int devOp, uint64_t redArg, int coll, int* blocks) {
   switch (dt) {
-    case 0: return resident_blocks_per_cu_dt0(devOp, redArg, blocks);
-    case 1: return resident_blocks_per_cu_dt1(devOp, redArg, blocks);
-    case 2: return resident_blocks_per_cu_dt2(devOp, redArg, blocks);
-    case 3: return resident_blocks_per_cu_dt3(devOp, redArg, blocks);
-    case 4: return resident_blocks_per_cu_dt4(devOp, redArg, blocks);
-    case 5: return resident_blocks_per_cu_dt5(devOp, redArg, blocks);
-    case 6: return resident_blocks_per_cu_dt6(devOp, redArg, blocks);
-    case 7: return resident_blocks_per_cu_dt7(devOp, redArg, blocks);
-    case 8: return resident_blocks_per_cu_dt8(devOp, redArg, blocks);
-    case 9: return resident_blocks_per_cu_dt9(devOp, redArg, blocks);
+    case 0: return resident_blocks_per_cu_dt0(devOp, redArg, coll, blocks);
+    case 1: return resident_blocks_per_cu_dt1(devOp, redArg, coll, blocks);
+    case 2: return resident_blocks_per_cu_dt2(devOp, redArg, coll, blocks);
+    case 3: return resident_blocks_per_cu_dt3(devOp, redArg, coll, blocks);
+    case 4: return resident_blocks_per_cu_dt4(devOp, redArg, coll, blocks);
+    case 5: return resident_blocks_per_cu_dt5(devOp, redArg, coll, blocks);
+    case 6: return resident_blocks_per_cu_dt6(devOp, redArg, coll, blocks);
+    case 7: return resident_blocks_per_cu_dt7(devOp, redArg, coll, blocks);
+    case 8: return resident_blocks_per_cu_dt8(devOp, redArg, coll, blocks);
+    case 9: return resident_blocks_per_cu_dt9(devOp, redArg, coll, blocks);
   }
   return hipErrorInvalidValue;
 }

@@ -76,7 +76,7 @@ struct ResScalars {
 };
 
 struct ResShared {
-  uint64_t recvStep, sendStep;
+  uint64_t recvStep[3], sendStep[3];
   int ok;
 };
 
@@ -95,17 +95,21 @@ __device__ __forceinline__ void st_bytes(char* p, uint32_t n, u32x4 v) {
     if ((uint32_t)k < n) p[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
 }
 
-// One workgroup's piece of a slice: srcs = [user src if US] + [recv FIFO if R], dsts = [user dst if
-// UD] + [send FIFO if S] (genericOp's order, prims_simple.h:131-132, :238-242), `bytes` bytes.
-// FIFO pieces start 16-byte aligned and own their slot up to the next 16 bytes, so a partial last
-// pack moves whole there; user buffers get exactly their bytes.
-template <int D, int OP, bool IsMin, bool US, bool R, bool UD, bool S>
-__device__ __forceinline__ void piece(const char* usrc, const char* rfifo, char* udst, char* sfifo, uint64_t bytes,
-                                      const Fold<D, OP, (int)US + (int)R, IsMin>& f) {
-  constexpr int K = (int)US + (int)R;
+// One workgroup's piece of a slice: srcs = [user src if US] + NR recv FIFOs, dsts = [user dst if UD]
+// + NS send FIFOs (genericOp's order, prims_simple.h:131-132, :238-242), `bytes` bytes. FIFO pieces
+// start 16-byte aligned and own their slot up to the next 16 bytes, so a partial last pack moves
+// whole there; user buffers get exactly their bytes.
+template <int N> using PtrArr = const char* [N > 0 ? N : 1];
+template <int D, int OP, bool IsMin, bool US, int NR, bool UD, int NS>
+__device__ __forceinline__ void piece(const char* usrc, const PtrArr<NR>& rfifo, char* udst, const PtrArr<NS>& sfifo,
+                                      uint64_t bytes, const Fold<D, OP, (int)US + NR, IsMin>& f) {
+  constexpr int K = (int)US + NR;
   const uint64_t rbytes = (bytes + 15) & ~15ull;
-  const __amdgpu_buffer_rsrc_t rr = res_rsrc(rfifo, R ? rbytes : 0);
-  const __amdgpu_buffer_rsrc_t sr = res_rsrc(sfifo, S ? rbytes : 0);
+  __amdgpu_buffer_rsrc_t rr[NR > 0 ? NR : 1], sr[NS > 0 ? NS : 1];
+#pragma unroll
+  for (int i = 0; i < NR; i++) rr[i] = res_rsrc(rfifo[i], rbytes);
+#pragma unroll
+  for (int i = 0; i < NS; i++) sr[i] = res_rsrc(sfifo[i], rbytes);
   const uint64_t nFull = bytes / 16;
   constexpr uint64_t kPass = (uint64_t)kBlock * kResU;
   uint64_t base = 0;
@@ -115,14 +119,16 @@ __device__ __forceinline__ void piece(const char* usrc, const char* rfifo, char*
     for (int u = 0; u < kResU; u++) {
       const uint64_t j = base + u * kBlock + threadIdx.x;
       if constexpr (US) in[u][0] = ld16<kPolPlain>(usrc + j * 16);
-      if constexpr (R) in[u][K - 1] = fifo_ld(rr, (uint32_t)(j * 16));
+#pragma unroll
+      for (int i = 0; i < NR; i++) in[u][(int)US + i] = fifo_ld(rr[i], (uint32_t)(j * 16));
     }
 #pragma unroll
     for (int u = 0; u < kResU; u++) {
       const uint64_t j = base + u * kBlock + threadIdx.x;
       const u32x4 out = f.run(in[u]);
       if constexpr (UD) st16<kPolPlain>(udst + j * 16, out);
-      if constexpr (S) fifo_st(sr, (uint32_t)(j * 16), out);
+#pragma unroll
+      for (int i = 0; i < NS; i++) fifo_st(sr[i], (uint32_t)(j * 16), out);
     }
   }
   const uint64_t nPacks = (bytes + 15) / 16;
@@ -130,31 +136,36 @@ __device__ __forceinline__ void piece(const char* usrc, const char* rfifo, char*
     const uint32_t valid = j < nFull ? 16u : (uint32_t)(bytes - nFull * 16);
     u32x4 in[K];
     if constexpr (US) in[0] = valid == 16 ? ld16<kPolPlain>(usrc + j * 16) : ld_bytes(usrc + j * 16, valid);
-    if constexpr (R) in[K - 1] = fifo_ld(rr, (uint32_t)(j * 16));
+#pragma unroll
+    for (int i = 0; i < NR; i++) in[(int)US + i] = fifo_ld(rr[i], (uint32_t)(j * 16));
     const u32x4 out = f.run(in);
     if constexpr (UD) {
       if (valid == 16) st16<kPolPlain>(udst + j * 16, out);
       else st_bytes(udst + j * 16, valid, out);
     }
-    if constexpr (S) fifo_st(sr, (uint32_t)(j * 16), out);
+#pragma unroll
+    for (int i = 0; i < NS; i++) fifo_st(sr[i], (uint32_t)(j * 16), out);
   }
 }
 
-// One rank's Primitives for one (channel, team member): step counters, connections, user buffers.
-template <int D, int OP, bool IsMin>
+// One rank's Primitives for one (channel, team member): up to MR recv and MS send connections (the
+// ring has one of each; the tree's FanAsymmetric / FanSymmetric up to NCCL_MAX_TREE_ARITY = 3),
+// their step counters, and the user buffers.
+template <int D, int OP, bool IsMin, int MR, int MS>
 struct ResPrims {
   static constexpr int esz = 16 / Ty<D>::EPP;
   ResScalars a;  // by value: a reference to the kernel argument would copy it to scratch
   const char* input;
   char* output;
-  char* recvFifo;
-  char* sendFifo;
-  char* recvTail;  // this member's record on this rank's device
-  char* recvHead;
-  char* sendTail;  // this member's record on the next rank's device
-  char* sendHead;
-  uint64_t recvStep, sendStep;
   int member;
+  int nRecv, nSend;
+  const char* recvFifo[MR];
+  char* recvTail[MR];  // this member's records of the connections into this rank
+  char* recvHead[MR];
+  const char* sendFifo[MS];
+  char* sendTail[MS];  // this member's records of the connections out of it (on the peers' GPUs)
+  char* sendHead[MS];
+  uint64_t recvStep[MR], sendStep[MS];
   ResShared* sh;  // the wait's outcome and the attached steps, broadcast from thread 0
 
   // waitPeer's spin (prims_simple.h:116-123), thread 0 only, bounded like checkAbort
@@ -181,24 +192,55 @@ struct ResPrims {
   __device__ __forceinline__ void attach() {
     if (threadIdx.x == 0) {
       const uint64_t cs = (uint64_t)(a.stepPerSlice * a.slicePerChunk);
-      const uint64_t rs = (ctr_ld(recvHead) + cs - 1) / cs * cs;
-      const uint64_t ss = (ctr_ld(sendTail) + cs - 1) / cs * cs;
-      ctr_st(recvHead, rs);
-      sh->recvStep = rs;
-      sh->sendStep = ss;
+#pragma unroll
+      for (int i = 0; i < MR; i++) {  // static indices: a private array indexed at run time spills
+        if (i < nRecv) {
+          const uint64_t rs = (ctr_ld(recvHead[i]) + cs - 1) / cs * cs;
+          ctr_st(recvHead[i], rs);
+          sh->recvStep[i] = rs;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MS; i++)
+        if (i < nSend) sh->sendStep[i] = (ctr_ld(sendTail[i]) + cs - 1) / cs * cs;
     }
     __syncthreads();
-    recvStep = sh->recvStep;
-    sendStep = sh->sendStep;
+#pragma unroll
+    for (int i = 0; i < MR; i++) recvStep[i] = i < nRecv ? sh->recvStep[i] : 0;
+#pragma unroll
+    for (int i = 0; i < MS; i++) sendStep[i] = i < nSend ? sh->sendStep[i] : 0;
     __syncthreads();
   }
 
-  // genericOp<0, 0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330) for this member's pieces.
+  // genericOp<0, 0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330) for this member's pieces:
+  // Recv = every recv connection, Send = every send connection.
   template <bool US, bool R, bool UD, bool S>
   __device__ __forceinline__ bool op(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
-    constexpr int K = (int)US + (int)R;
-    // PreOpSrcs = SrcBuf == Input (prims_simple.h:279-280), preOpArgs = redOpArgs
-    const Fold<D, OP, K, IsMin> f(a.redArg, US ? 1 : 0, postOp, a.redArg);
+    const int nr = R ? nRecv : 0;
+    if (nr == 0) return opS<US, 0, UD, S>(srcIx, dstIx, nelem, postOp);
+    if constexpr (MR >= 2) {
+      if (nr == 2) return opS<US, 2, UD, S>(srcIx, dstIx, nelem, postOp);
+    }
+    if constexpr (MR >= 3) {
+      if (nr == 3) return opS<US, 3, UD, S>(srcIx, dstIx, nelem, postOp);
+    }
+    return opS<US, 1, UD, S>(srcIx, dstIx, nelem, postOp);
+  }
+  template <bool US, int NR, bool UD, bool S>
+  __device__ __forceinline__ bool opS(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
+    const int ns = S ? nSend : 0;
+    if (ns == 0) return opN<US, NR, UD, 0>(srcIx, dstIx, nelem, postOp);
+    if constexpr (MS >= 2) {
+      if (ns == 2) return opN<US, NR, UD, 2>(srcIx, dstIx, nelem, postOp);
+    }
+    if constexpr (MS >= 3) {
+      if (ns == 3) return opN<US, NR, UD, 3>(srcIx, dstIx, nelem, postOp);
+    }
+    return opN<US, NR, UD, 1>(srcIx, dstIx, nelem, postOp);
+  }
+  template <bool US, int NR, bool UD, int NS>
+  __device__ __forceinline__ bool opN(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
+    constexpr int K = (int)US + NR;
     nelem = nelem < 0 ? 0 : nelem;
     int64_t sliceSize = a.stepElems * a.stepPerSlice;
     sliceSize = imax(divUp64(nelem, 16 * (int64_t)a.slicePerChunk) * 16, sliceSize / 32);
@@ -208,8 +250,11 @@ struct ResPrims {
       if (sliceSize < 0) sliceSize = 0;
       if (threadIdx.x == 0) {
         bool ok = true;
-        if (R) ok = wait_ge(recvTail, recvStep + a.stepPerSlice);
-        if (ok && S && sendStep + a.stepPerSlice > 8) ok = wait_ge(sendHead, sendStep + a.stepPerSlice - 8);
+#pragma unroll
+        for (int i = 0; i < NR; i++) ok = ok && wait_ge(recvTail[i], recvStep[i] + a.stepPerSlice);
+#pragma unroll
+        for (int i = 0; i < NS; i++)
+          if (ok && sendStep[i] + a.stepPerSlice > 8) ok = wait_ge(sendHead[i], sendStep[i] + a.stepPerSlice - 8);
         sh->ok = ok ? 1 : 0;
       }
       __syncthreads();  // the other waves load the handed-off bytes only behind the poll
@@ -222,13 +267,21 @@ struct ResPrims {
       constexpr int64_t epp = 16 / esz;
       const int64_t per = divUp64(divUp64(a.stepElems * a.stepPerSlice, a.team), epp) * epp;
       const int64_t lo = imin(sliceSize, per * member), hi = imin(sliceSize, lo + per);
-      if (hi > lo && K > 0 && ((int)UD + (int)S) > 0) {
+      if constexpr (K > 0 && ((int)UD + NS) > 0) {  // else no data moves (genericOp's k > 0 && m > 0)
+        if (hi > lo) {
+        // PreOpSrcs = SrcBuf == Input (prims_simple.h:279-280), preOpArgs = redOpArgs
+        const Fold<D, OP, K, IsMin> f(a.redArg, US ? 1 : 0, postOp, a.redArg);
         const uint64_t slotOff = (uint64_t)lo * esz;
-        piece<D, OP, IsMin, US, R, UD, S>(
-            US ? input + (srcIx + offset + lo) * esz : nullptr,
-            R ? recvFifo + (recvStep % 8) * a.stepBytes + slotOff : nullptr,
-            UD ? output + (dstIx + offset + lo) * esz : nullptr,
-            S ? sendFifo + (sendStep % 8) * a.stepBytes + slotOff : nullptr, (uint64_t)(hi - lo) * esz, f);
+        const char* rf[NR > 0 ? NR : 1];
+        const char* sf[NS > 0 ? NS : 1];
+#pragma unroll
+        for (int i = 0; i < NR; i++) rf[i] = recvFifo[i] + (recvStep[i] % 8) * a.stepBytes + slotOff;
+#pragma unroll
+        for (int i = 0; i < NS; i++) sf[i] = sendFifo[i] + (sendStep[i] % 8) * a.stepBytes + slotOff;
+        piece<D, OP, IsMin, US, NR, UD, NS>(US ? input + (srcIx + offset + lo) * esz : nullptr, rf,
+                                            UD ? output + (dstIx + offset + lo) * esz : nullptr, sf,
+                                            (uint64_t)(hi - lo) * esz, f);
+        }
       }
       // postPeer (prims_simple.h:177-188): every wave's FIFO stores acknowledged and FIFO loads
       // returned, then one lane posts for the workgroup. FIFO bytes are written and read only with
@@ -236,11 +289,15 @@ struct ResPrims {
       // "sc1 stores and loads both sides" of MI355X_MICROARCH.md, Guideline 16).
       drain();
       __syncthreads();
-      if (R) recvStep += a.stepPerSlice;
-      if (S) sendStep += a.stepPerSlice;
+#pragma unroll
+      for (int i = 0; i < NR; i++) recvStep[i] += a.stepPerSlice;
+#pragma unroll
+      for (int i = 0; i < NS; i++) sendStep[i] += a.stepPerSlice;
       if (threadIdx.x == 0) {
-        if (R) ctr_st(recvHead, recvStep);
-        if (S) ctr_st(sendTail, sendStep);
+#pragma unroll
+        for (int i = 0; i < NR; i++) ctr_st(recvHead[i], recvStep[i]);
+#pragma unroll
+        for (int i = 0; i < NS; i++) ctr_st(sendTail[i], sendStep[i]);
       }
       offset += sliceSize;
     }
@@ -248,16 +305,19 @@ struct ResPrims {
   }
 };
 
+template <int D, int OP, bool IsMin>
+using RingPrims = ResPrims<D, OP, IsMin, 1, 1>;
+
 // runRing for ncclAllReduce (all_reduce.h:12-84), one rank's view of one channel part. Primitive
 // shapes op<user src, recv, user dst, send>: sendInput <1,0,0,1>, recvReduceSend <1,1,0,1>,
 // recvReduceCopySend <1,1,1,1>, recvCopySend <0,1,1,1>, recvOutput <0,1,1,0>, recvReduceCopy <1,1,1,0>,
 // copySend <1,0,1,1> (prims_simple.h:897-976).
 template <int D, int OP, bool IsMin>
-__device__ __forceinline__ void run_all_reduce(ResPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_all_reduce(RingPrims<D, OP, IsMin>& p, int rank, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks;
   int64_t chunkCount = p.a.chunkCount;
   const int64_t loopCount = nranks * chunkCount;
-  constexpr int64_t epp = 16 / ResPrims<D, OP, IsMin>::esz;
+  constexpr int64_t epp = 16 / RingPrims<D, OP, IsMin>::esz;
   auto modRanks = [&](int r) { return r - (r >= nranks ? nranks : 0); };
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += loopCount) {
     const int64_t remCount = partCount - elemOffset;
@@ -288,7 +348,7 @@ __device__ __forceinline__ void run_all_reduce(ResPrims<D, OP, IsMin>& p, int ra
 // runRing for ncclReduceScatter (reduce_scatter.h:12-52): a.count is the per-rank recvcount; rank
 // d's segment starts at d * count in every sendbuff.
 template <int D, int OP, bool IsMin>
-__device__ __forceinline__ void run_reduce_scatter(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_reduce_scatter(RingPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks;
   const int64_t count = p.a.count, chunkCount = p.a.chunkCount;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += chunkCount) {
@@ -307,8 +367,8 @@ __device__ __forceinline__ void run_reduce_scatter(ResPrims<D, OP, IsMin>& p, in
 // runRing for ncclAllGather (all_gather.h:12-66): a.count is the per-rank sendcount; in place when
 // the input chunk already sits at its place in the output (:52-56).
 template <int D, int OP, bool IsMin>
-__device__ __forceinline__ void run_all_gather(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
-  constexpr int esz = ResPrims<D, OP, IsMin>::esz;
+__device__ __forceinline__ void run_all_gather(RingPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+  constexpr int esz = RingPrims<D, OP, IsMin>::esz;
   const int nranks = p.a.nRanks;
   const int64_t count = p.a.count, chunkCount = p.a.chunkCount;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += chunkCount) {
@@ -330,7 +390,7 @@ __device__ __forceinline__ void run_all_gather(ResPrims<D, OP, IsMin>& p, int r,
 
 // runRing for ncclReduce (reduce.h:12-50) and ncclBroadcast (broadcast.h:12-58), ProtoSimple<1,1>.
 template <int D, int OP, bool IsMin>
-__device__ __forceinline__ void run_reduce(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_reduce(RingPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks, root = p.a.root, prevRank = (r + nranks - 1) % nranks;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += p.a.chunkCount) {
     const int64_t offset = partOffset + elemOffset;
@@ -343,7 +403,7 @@ __device__ __forceinline__ void run_reduce(ResPrims<D, OP, IsMin>& p, int r, int
   }
 }
 template <int D, int OP, bool IsMin>
-__device__ __forceinline__ void run_broadcast(ResPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
+__device__ __forceinline__ void run_broadcast(RingPrims<D, OP, IsMin>& p, int r, int64_t partOffset, int64_t partCount) {
   const int nranks = p.a.nRanks, root = p.a.root, nextRank = (r + 1) % nranks;
   for (int64_t elemOffset = 0; elemOffset < partCount; elemOffset += p.a.chunkCount) {
     const int64_t offset = partOffset + elemOffset;
@@ -359,23 +419,29 @@ __device__ __forceinline__ void run_broadcast(ResPrims<D, OP, IsMin>& p, int r, 
 }
 
 template <int D, int OP, bool IsMin>
+__device__ __forceinline__ ResScalars scalars_of(const ResParams& a) {
+  return {a.chunkCount, a.stepElems, a.count, a.stepBytes, a.redArg, a.timeoutTicks, a.status,
+          a.stepPerSlice, a.slicePerChunk, a.team, a.nRanks, a.root};
+}
+
+template <int D, int OP, bool IsMin>
 __global__ __launch_bounds__(kBlock) void ring_resident(ResParams a) {
   __shared__ ResShared sh;
   const int member = blockIdx.x % a.team;
   const int part = (blockIdx.x / a.team) % a.nParts;
   const int rank = a.rankOf[blockIdx.x / (a.team * a.nParts)];
   const ResConn& c = a.conns[a.partChannel[part] * a.nRanks + rank];
-  ResPrims<D, OP, IsMin> p{{a.chunkCount, a.stepElems, a.count, a.stepBytes, a.redArg, a.timeoutTicks, a.status,
-                            a.stepPerSlice, a.slicePerChunk, a.team, a.nRanks, a.root}};
+  RingPrims<D, OP, IsMin> p{scalars_of<D, OP, IsMin>(a)};
   p.input = a.input[rank];
   p.output = a.output[rank];
-  p.recvFifo = c.recvFifo;
-  p.sendFifo = c.sendFifo;
-  p.recvTail = c.recvCtr + (size_t)member * kResCtrBytes;
-  p.recvHead = p.recvTail + kResHeadOff;
-  p.sendTail = c.sendCtr + (size_t)member * kResCtrBytes;
-  p.sendHead = p.sendTail + kResHeadOff;
   p.member = member;
+  p.nRecv = p.nSend = 1;
+  p.recvFifo[0] = c.recvFifo;
+  p.sendFifo[0] = c.sendFifo;
+  p.recvTail[0] = c.recvCtr + (size_t)member * kResCtrBytes;
+  p.recvHead[0] = p.recvTail[0] + kResHeadOff;
+  p.sendTail[0] = c.sendCtr + (size_t)member * kResCtrBytes;
+  p.sendHead[0] = p.sendTail[0] + kResHeadOff;
   p.sh = &sh;
   p.attach();
   const int64_t off = a.partOffset[part], cnt = a.partCount[part];
@@ -388,23 +454,86 @@ __global__ __launch_bounds__(kBlock) void ring_resident(ResParams a) {
   }
 }
 
-template <int D, int OP>
-static const void* kernel_op(uint64_t redArg) {
-  if constexpr (OP == nexrDevMinMax) {
-    if ((redArg & 1) == 0) return (const void*)&ring_resident<D, OP, true>;  // isMin, reduce_kernel.h:64
+// runTreeSplit for ncclAllReduce (all_reduce.h:150-230), ProtoSimple<1,1>. Each (rank, channel) has
+// two teams, as the reference splits a block's threads: role 0 reduces up (recv from the children,
+// send to the parent: FanAsymmetric<3,1>), role 1 broadcasts down (recv from the parent, send to the
+// children: FanAsymmetric<1,3>). The root's role 0 does both in one recvReduceCopySend over its
+// children (FanSymmetric<3>); its role 1 has nothing to do.
+template <int D, int OP, bool IsMin, int MR, int MS>
+__device__ __forceinline__ void tree_role(const ResParams& a, ResShared* sh, const ResTreeConn& t, int rank, int role,
+                                          int member, int64_t off, int64_t cnt) {
+  ResPrims<D, OP, IsMin, MR, MS> p{scalars_of<D, OP, IsMin>(a)};
+  p.input = a.input[rank];
+  p.output = a.output[rank];
+  p.member = member;
+  p.sh = sh;
+  const size_t m = (size_t)member * kResCtrBytes;
+  const bool up = role == 0;
+  p.nRecv = up ? t.nDown : 1;
+  p.nSend = up ? (t.root ? t.nDown : 1) : t.nDown;
+#pragma unroll
+  for (int i = 0; i < MR; i++) {  // unused entries are never dereferenced (nRecv / nSend bound every use)
+    p.recvFifo[i] = up ? t.upRecvFifo[i] : t.downRecvFifo;
+    p.recvTail[i] = (up ? t.upRecvCtr[i] : t.downRecvCtr) + m;
+    p.recvHead[i] = p.recvTail[i] + kResHeadOff;
   }
-  return (const void*)&ring_resident<D, OP, false>;
+#pragma unroll
+  for (int i = 0; i < MS; i++) {
+    p.sendFifo[i] = up && !t.root ? t.upSendFifo : t.downSendFifo[i];
+    p.sendTail[i] = (up && !t.root ? t.upSendCtr : t.downSendCtr[i]) + m;
+    p.sendHead[i] = p.sendTail[i] + kResHeadOff;
+  }
+  p.attach();
+  const bool leaf = t.nDown == 0;
+  for (int64_t elemOffset = 0; elemOffset < cnt; elemOffset += a.chunkCount) {
+    const int64_t offset = off + elemOffset;
+    const int64_t nelem = imin(a.chunkCount, cnt - elemOffset);
+    bool ok;
+    if (t.root) ok = p.template op<true, true, true, true>(offset, offset, nelem, true);
+    else if (up) ok = leaf ? p.template op<true, false, false, true>(offset, -1, nelem, false)
+                           : p.template op<true, true, false, true>(offset, -1, nelem, false);
+    else ok = leaf ? p.template op<false, true, true, false>(-1, offset, nelem, false)
+                   : p.template op<false, true, true, true>(-1, offset, nelem, false);
+    if (!ok) return;
+  }
+}
+
+template <int D, int OP, bool IsMin>
+__global__ __launch_bounds__(kBlock) void tree_resident(ResParams a) {
+  __shared__ ResShared sh;
+  const int member = blockIdx.x % a.team;
+  const int role = (blockIdx.x / a.team) % 2;
+  const int part = (blockIdx.x / (2 * a.team)) % a.nParts;
+  const int rank = a.rankOf[blockIdx.x / (2 * a.team * a.nParts)];
+  const ResTreeConn& t = a.tree[a.partChannel[part] * a.nRanks + rank];
+  const int64_t off = a.partOffset[part], cnt = a.partCount[part];
+  if (t.root) {
+    if (role == 0) tree_role<D, OP, IsMin, 3, 3>(a, &sh, t, rank, 0, member, off, cnt);
+  } else if (role == 0) {
+    tree_role<D, OP, IsMin, 3, 1>(a, &sh, t, rank, 0, member, off, cnt);
+  } else {
+    tree_role<D, OP, IsMin, 1, 3>(a, &sh, t, rank, 1, member, off, cnt);
+  }
+}
+
+template <int D, int OP>
+static const void* kernel_op(uint64_t redArg, bool tree) {
+  if constexpr (OP == nexrDevMinMax) {
+    if ((redArg & 1) == 0)  // isMin, reduce_kernel.h:64
+      return tree ? (const void*)&tree_resident<D, OP, true> : (const void*)&ring_resident<D, OP, true>;
+  }
+  return tree ? (const void*)&tree_resident<D, OP, false> : (const void*)&ring_resident<D, OP, false>;
 }
 
 template <int D>
-static const void* kernel_for(int op, uint64_t redArg) {
+static const void* kernel_for(int op, uint64_t redArg, bool tree) {
   switch (op) {
-    case nexrDevSum: return kernel_op<D, nexrDevSum>(redArg);
-    case nexrDevProd: return kernel_op<D, nexrDevProd>(redArg);
-    case nexrDevMinMax: return kernel_op<D, nexrDevMinMax>(redArg);
-    case nexrDevPreMulSum: return kernel_op<D, nexrDevPreMulSum>(redArg);
+    case nexrDevSum: return kernel_op<D, nexrDevSum>(redArg, tree);
+    case nexrDevProd: return kernel_op<D, nexrDevProd>(redArg, tree);
+    case nexrDevMinMax: return kernel_op<D, nexrDevMinMax>(redArg, tree);
+    case nexrDevPreMulSum: return kernel_op<D, nexrDevPreMulSum>(redArg, tree);
     case nexrDevSumPostDiv:
-      if constexpr (Ty<D>::kIsInt) return kernel_op<D, nexrDevSumPostDiv>(redArg);
+      if constexpr (Ty<D>::kIsInt) return kernel_op<D, nexrDevSumPostDiv>(redArg, tree);
       break;
   }
   return nullptr;
@@ -414,14 +543,14 @@ static const void* kernel_for(int op, uint64_t redArg) {
 #define NEXR_CAT(a, b) NEXR_CAT2(a, b)
 
 hipError_t NEXR_CAT(launch_resident_dt, NEXR_DT)(int op, const ResParams& p, int grid, hipStream_t s) {
-  const void* fn = kernel_for<NEXR_DT>(op, p.redArg);
+  const void* fn = kernel_for<NEXR_DT>(op, p.redArg, p.coll == kResTreeAllReduce);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {const_cast<ResParams*>(&p)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
 }
 
-hipError_t NEXR_CAT(resident_blocks_per_cu_dt, NEXR_DT)(int op, uint64_t redArg, int* blocks) {
-  const void* fn = kernel_for<NEXR_DT>(op, redArg);
+hipError_t NEXR_CAT(resident_blocks_per_cu_dt, NEXR_DT)(int op, uint64_t redArg, int coll, int* blocks) {
+  const void* fn = kernel_for<NEXR_DT>(op, redArg, coll == kResTreeAllReduce);
   if (!fn) return hipErrorInvalidValue;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fn, kBlock, 0);
 }

@@ -695,6 +695,12 @@ void freeResident(nexrRingComm* c) {
     (void)hipFree(c->resFifo[k]);
   }
   c->resFifo.clear();
+  for (auto* v : {&c->resTreeTable, &c->resTreeCtr, &c->resTreeFifo})
+    for (void* q : *v)
+      if (q) (void)hipFree(q);  // hipFree finds the owning device itself
+  c->resTreeTable.clear();
+  c->resTreeCtr.clear();
+  c->resTreeFifo.clear();
   c->resDevs.clear();
   c->resTable.clear();
   c->resCtr.clear();
@@ -713,6 +719,14 @@ int resDevIndex(const nexrRingComm* c, int rank) {
 // (hipDeviceMallocUncached, as RCCL allocates its P2P FIFOs and flags): their writers then sit on
 // another GPU, whose stores the owner's L2 does not see. On one GPU the communicator's own FIFOs
 // serve, and the records are ordinary device memory.
+bool residentMulti(const nexrRingComm* c) {
+  static const bool forceUncached = [] {  // NEXR_RESIDENT_UNCACHED=1: the multi-GPU layout on one GPU (tests)
+    const char* v = getenv("NEXR_RESIDENT_UNCACHED");
+    return v && v[0] == '1';
+  }();
+  return c->resDevs.size() > 1 || forceUncached;
+}
+
 nexrResult_t ensureResident(nexrRingComm* c) {
   if (!c->resDevs.empty()) return nexrSuccess;
   const int n = c->cfg.nRanks, nCh = c->cfg.nChannels;
@@ -724,11 +738,7 @@ nexrResult_t ensureResident(nexrRingComm* c) {
   c->resCtr.assign(nd, nullptr);
   c->resStatus.assign(nd, nullptr);
   const size_t ctrBytes = (size_t)nCh * n * nexr::kResMaxTeam * nexr::kResCtrBytes;
-  static const bool forceUncached = [] {  // NEXR_RESIDENT_UNCACHED=1: the multi-GPU layout on one GPU (tests)
-    const char* v = getenv("NEXR_RESIDENT_UNCACHED");
-    return v && v[0] == '1';
-  }();
-  const bool multi = nd > 1 || forceUncached;
+  const bool multi = residentMulti(c);
   auto devAlloc = [&](void** p, size_t bytes) {
     return multi ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) : hipMalloc(p, bytes);
   };
@@ -777,6 +787,87 @@ nexrResult_t ensureResident(nexrRingComm* c) {
   return nexrSuccess;
 }
 
+// First tree call (after ensureResident): every channel's tree links (ensureTree), per device a
+// zeroed record block for the tree's connections and the (channel, rank) ResTreeConn table. The
+// record and FIFO of up[r] sit on the parent's GPU, those of down[r] on r's.
+nexrResult_t ensureResidentTree(nexrRingComm* c, bool multi) {
+  if (!c->resTreeTable.empty()) return nexrSuccess;
+  const int n = c->cfg.nRanks, nCh = c->cfg.nChannels;
+  for (int ch = 0; ch < nCh; ch++) {
+    nexrResult_t r = ensureTree(channelComm(c, ch));
+    if (r != nexrSuccess) return r;
+  }
+  const size_t nd = c->resDevs.size();
+  c->resTreeTable.assign(nd, nullptr);
+  c->resTreeCtr.assign(nd, nullptr);
+  const size_t ctrBytes = (size_t)nCh * 2 * n * nexr::kResMaxTeam * nexr::kResCtrBytes;
+  auto devAlloc = [&](void** p, size_t bytes) {
+    return multi ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) : hipMalloc(p, bytes);
+  };
+  auto fail = [&] {
+    freeResident(c);
+    return nexrUnhandledCudaError;
+  };
+  for (size_t i = 0; i < nd; i++) {
+    if (hipSetDevice(c->resDevs[i]) != hipSuccess || devAlloc(&c->resTreeCtr[i], ctrBytes) != hipSuccess ||
+        hipMemset(c->resTreeCtr[i], 0, ctrBytes) != hipSuccess ||
+        hipMalloc(&c->resTreeTable[i], sizeof(nexr::ResTreeConn) * nCh * n) != hipSuccess)
+      return fail();
+  }
+  // receiver of connection id (r: up[r], n + r: down[r]) on channel ch
+  auto receiver = [&](int ch, int id) { return id < n ? channelComm(c, ch)->tree[id].up : id - n; };
+  if (multi) {
+    c->resTreeFifo.assign((size_t)nCh * 2 * n, nullptr);
+    for (int ch = 0; ch < nCh; ch++)
+      for (int id = 0; id < 2 * n; id++) {
+        const int rcv = receiver(ch, id);
+        if (rcv < 0) continue;  // up[root]
+        if (hipSetDevice(c->devices[rcv]) != hipSuccess ||
+            devAlloc(&c->resTreeFifo[(size_t)ch * 2 * n + id], c->cfg.buffBytes) != hipSuccess)
+          return fail();
+      }
+  }
+  auto fifo = [&](int ch, int id) -> char* {
+    if (multi) return (char*)c->resTreeFifo[(size_t)ch * 2 * n + id];
+    nexrRingComm* ck = channelComm(c, ch);
+    return id < n ? ck->treeUp[id]->fifo : ck->treeDown[id - n]->fifo;
+  };
+  auto rec = [&](int ch, int id) {
+    return (char*)c->resTreeCtr[resDevIndex(c, receiver(ch, id))] +
+           ((size_t)(ch * 2 * n + id) * nexr::kResMaxTeam) * nexr::kResCtrBytes;
+  };
+  std::vector<nexr::ResTreeConn> table((size_t)nCh * n);
+  for (int ch = 0; ch < nCh; ch++) {
+    const std::vector<TreeLinks>& tl = channelComm(c, ch)->tree;
+    for (int r = 0; r < n; r++) {
+      nexr::ResTreeConn t{};
+      t.nDown = tl[r].nDown();
+      t.root = tl[r].up < 0 ? 1 : 0;
+      for (int i = 0; i < t.nDown; i++) {
+        const int child = tl[r].down[i];
+        t.upRecvFifo[i] = fifo(ch, child);
+        t.upRecvCtr[i] = rec(ch, child);
+        t.downSendFifo[i] = fifo(ch, n + child);
+        t.downSendCtr[i] = rec(ch, n + child);
+      }
+      if (!t.root) {
+        t.upSendFifo = fifo(ch, r);
+        t.upSendCtr = rec(ch, r);
+        t.downRecvFifo = fifo(ch, n + r);
+        t.downRecvCtr = rec(ch, n + r);
+      }
+      table[(size_t)ch * n + r] = t;
+    }
+  }
+  for (size_t i = 0; i < nd; i++) {
+    if (hipSetDevice(c->resDevs[i]) != hipSuccess ||
+        hipMemcpy(c->resTreeTable[i], table.data(), sizeof(nexr::ResTreeConn) * table.size(), hipMemcpyHostToDevice) !=
+            hipSuccess)
+      return fail();
+  }
+  return nexrSuccess;
+}
+
 // Workgroups per (rank, channel): NEXR_RESIDENT_TEAM, else as many as give every member at least
 // 16 KiB of a full slice (StepPerSlice steps), at most about 512 workgroups on the busiest device (two
 // per CU) and at most kResMaxTeam. Measured on MI355X (tools/resident_time.py, 2 ranks, 256 MiB):
@@ -792,7 +883,7 @@ int residentTeam(int ranksOnDevice, int nParts, size_t sliceBytes) {
 }
 
 nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* const* sendbuffs, void* const* recvbuffs,
-                                size_t count, int datatype, int op, int root) {
+                                size_t count, int datatype, int op, int root, bool tree = false) {
   if (!c || c->peer) return nexrInvalidArgument;
   if (c->cfg.memMode != nexrRingDeviceMemory || c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
   int sem = nexrSemanticsNccl;
@@ -817,12 +908,14 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
   if (sem == nexrSemanticsFork && red.op == nexrDevMinMax)
     kdt = datatype == nexrInt8 ? nexrUint8 : datatype == nexrInt32 ? nexrUint32 : datatype == nexrInt64 ? nexrUint64 : datatype;
   r = ensureResident(c);
+  if (r == nexrSuccess && tree) r = ensureResidentTree(c, residentMulti(c));
   if (r != nexrSuccess) return r;
-  const Geom g = (coll == kReduce || coll == kBroadcast) ? kGeomPipe : kGeomRing;
+  const Geom g = (coll == kReduce || coll == kBroadcast || tree) ? kGeomPipe : kGeomRing;
   const int trafficPerByte = coll == kAllReduce ? 2 : (coll == kReduceScatter || coll == kAllGather) ? n : 1;
   std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, trafficPerByte);
   nexr::ResParams a{};
-  a.coll = coll == kAllReduce       ? nexr::kResAllReduce
+  a.coll = tree                     ? nexr::kResTreeAllReduce
+           : coll == kAllReduce     ? nexr::kResAllReduce
            : coll == kReduceScatter ? nexr::kResReduceScatter
            : coll == kAllGather     ? nexr::kResAllGather
            : coll == kReduce        ? nexr::kResReduce
@@ -836,7 +929,8 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
     a.partCount[i] = parts[i].count;
     a.partChannel[i] = parts[i].channel;
   }
-  a.chunkCount = chunkElems(c, g, esz, false, 0);
+  // calcCollChunking per part (enqueue.cc:1993-1999); for SIMPLE every part gets the same chunk
+  a.chunkCount = chunkElems(c, g, esz, tree, parts.empty() ? 0 : (size_t)parts[0].count * esz);
   a.stepElems = (int64_t)(c->stepBytes / esz);
   a.stepBytes = c->stepBytes;
   a.stepPerSlice = g.sliceSteps;
@@ -851,28 +945,31 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
   std::vector<std::vector<int>> onDev(c->resDevs.size());
   for (int i = 0; i < n; i++) onDev[resDevIndex(c, i)].push_back(i);
   for (const auto& v : onDev) busiest = std::max(busiest, (int)v.size());
-  a.team = residentTeam(busiest, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
+  const int roles = tree ? 2 : 1;  // the tree's reduce-up and broadcast-down teams
+  a.team = residentTeam(busiest * roles, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
   // Every workgroup of a device's grid must be resident at once (a rank's workgroups wait on others'):
   // the team shrinks to what the kernel's occupancy allows on every device used.
   long capacity = -1;
   for (size_t d = 0; d < c->resDevs.size(); d++) {
     int perCU = 0, cus = 0;
-    if (hipSetDevice(c->resDevs[d]) != hipSuccess || nexr::resident_blocks_per_cu(kdt, red.op, red.scalarArg, &perCU) != hipSuccess ||
+    if (hipSetDevice(c->resDevs[d]) != hipSuccess ||
+        nexr::resident_blocks_per_cu(kdt, red.op, red.scalarArg, a.coll, &perCU) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->resDevs[d]) != hipSuccess)
       return nexrUnhandledCudaError;
     const long cap = (long)perCU * cus;
     capacity = capacity < 0 ? cap : std::min(capacity, cap);
   }
-  if ((long)busiest * a.nParts * a.team > capacity) a.team = (int)(capacity / ((long)busiest * a.nParts));
+  if ((long)busiest * roles * a.nParts * a.team > capacity) a.team = (int)(capacity / ((long)busiest * roles * a.nParts));
   if (a.team < 1) return nexrInvalidUsage;
   std::vector<hipStream_t> used;
   for (size_t d = 0; d < onDev.size() && r == nexrSuccess; d++) {
     a.conns = (const nexr::ResConn*)c->resTable[d];
+    a.tree = tree ? (const nexr::ResTreeConn*)c->resTreeTable[d] : nullptr;
     a.status = c->resStatus[d];
     for (size_t k = 0; k < onDev[d].size(); k++) a.rankOf[k] = onDev[d][k];
     hipStream_t s = c->streams[onDev[d][0]];
     if (hipSetDevice(c->resDevs[d]) != hipSuccess ||
-        nexr::launch_resident(kdt, red.op, a, (int)onDev[d].size() * a.nParts * a.team, s) != hipSuccess)
+        nexr::launch_resident(kdt, red.op, a, (int)onDev[d].size() * roles * a.nParts * a.team, s) != hipSuccess)
       r = nexrUnhandledCudaError;
     else
       used.push_back(s);
@@ -896,6 +993,12 @@ NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t c, const void* co
                                                 void* const* recvbuffs, size_t count, int datatype, int op) {
   DeviceGuard dg(c && c->needHip);
   return residentCollective(c, kAllReduce, sendbuffs, recvbuffs, count, datatype, op, 0);
+}
+
+NEXR_API nexrResult_t nexrTreeAllReduceResident(nexrRingComm_t c, const void* const* sendbuffs,
+                                                void* const* recvbuffs, size_t count, int datatype, int op) {
+  DeviceGuard dg(c && c->needHip);
+  return residentCollective(c, kAllReduce, sendbuffs, recvbuffs, count, datatype, op, 0, /*tree=*/true);
 }
 
 NEXR_API nexrResult_t nexrRingReduceScatterResident(nexrRingComm_t c, const void* const* sendbuffs,

@@ -22,7 +22,7 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
                     "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv",
                     "nexrRingAllReduceResident", "nexrRingReduceScatterResident", "nexrRingAllGatherResident",
-                    "nexrRingReduceResident", "nexrRingBroadcastResident")
+                    "nexrRingReduceResident", "nexrRingBroadcastResident", "nexrTreeAllReduceResident")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -66,6 +66,8 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingAllReduce.restype = ctypes.c_int
         L.nexrRingAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
         L.nexrRingAllReduceResident.restype = ctypes.c_int
+        L.nexrTreeAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
+        L.nexrTreeAllReduceResident.restype = ctypes.c_int
         _arr, _i, _sz = ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t
         for f, extra in ((L.nexrRingReduceScatterResident, [_i, _i]), (L.nexrRingAllGatherResident, [_i]),
                          (L.nexrRingReduceResident, [_i, _i, _i]), (L.nexrRingBroadcastResident, [_i, _i])):
@@ -153,6 +155,11 @@ class RingComm:
         s, r = self._arrays(sendbuffs, recvbuffs)
         _check(ring_lib().nexrRingAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
                "nexrRingAllReduceResident")
+
+    def tree_all_reduce_resident(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int) -> None:
+        s, r = self._arrays(sendbuffs, recvbuffs)
+        _check(ring_lib().nexrTreeAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
+               "nexrTreeAllReduceResident")
 
     def reduce_scatter_resident(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)

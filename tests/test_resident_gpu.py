@@ -274,3 +274,32 @@ print("ok")
     env = dict(os.environ, NEXR_RESIDENT_TEAM="128")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("n,per_node,tree_index,dt,op,nch", [(2, 0, 0, mg.F32, SUM, 1), (5, 1, 0, mg.BF16, SUM, 1),
+                                                             (8, 2, 0, mg.F32, SUM, 2), (6, 1, 1, mg.I32, MIN, 1),
+                                                             (4, 0, 0, mg.F16, AVG, 4), (7, 1, 0, mg.F64, PROD, 2)])
+def test_resident_tree_all_reduce(ring, oracle, n, per_node, tree_index, dt, op, nch):
+    """runTreeSplit in one launch: reduce-up and broadcast-down teams per (rank, channel), fan-in up to
+    4 (a node head with 3 children), chain and double-binary-tree topologies, both trees (channels in
+    the upper half use the other one): equal to nexrTreeAllReduce on the same communicator, bit for
+    bit, and to the oracle where one channel makes its expectation channel-free."""
+    from oracle.ring import tree_allreduce_expected, tree_topology
+    count = 120_011
+    inputs = mg.gen_inputs(dt, n, count, 0x3300 + n + per_node, True)
+    send = _dev(inputs)
+    recv = [torch.zeros_like(s) for s in send]
+    host = [torch.zeros_like(s) for s in send]
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 1 << 16, tree_ranks_per_node=per_node, tree_index=tree_index,
+                       n_channels=nch, timeout_ms=20000) as comm:
+        comm.tree_all_reduce_resident(_ptrs(send), _ptrs(recv), count, dt, op)
+        comm.tree_all_reduce(_ptrs(send), _ptrs(host), count, dt, op)
+        again = [torch.zeros_like(s) for s in send]
+        comm.tree_all_reduce_resident(_ptrs(send), _ptrs(again), count, dt, op)  # counters resume
+    for r in range(n):
+        assert torch.equal(recv[r].view(torch.uint8), host[r].view(torch.uint8)), f"rank {r} vs host tree"
+        assert torch.equal(again[r].view(torch.uint8), host[r].view(torch.uint8)), f"rank {r}, second call"
+    if nch == 1:
+        exp = tree_allreduce_expected(inputs, dt, op, tree_topology(n, per_node, tree_index), "simple")
+        for r in range(n):
+            assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r} vs oracle"

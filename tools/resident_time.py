@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--channels", default="1,4")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--colls", action="store_true")
+    ap.add_argument("--tree", action="store_true", help="time the tree all-reduce (resident vs host) instead")
     args = ap.parse_args()
     import torch
     ring = importlib.import_module("nex-nccl_amd.ring")
@@ -39,7 +40,10 @@ def main():
                 sp, rp = [x.data_ptr() for x in xs], [y.data_ptr() for y in ys]
                 line = {"ranks": n, "channels": nch, "bytes_per_rank": nbytes}
                 with ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=20000) as comm:
-                    for name, fn in (("resident", comm.all_reduce_resident), ("host", comm.all_reduce)):
+                    pair = ((("resident", comm.tree_all_reduce_resident), ("host", comm.tree_all_reduce)) if args.tree
+                            else (("resident", comm.all_reduce_resident), ("host", comm.all_reduce)))
+                    line["algorithm"] = "tree" if args.tree else "ring"
+                    for name, fn in pair:
                         for y in ys:
                             y.zero_()
                         torch.cuda.synchronize()
