@@ -213,30 +213,38 @@ struct ResPrims {
   }
 
   // genericOp<0, 0, Recv, Send, SrcBuf, DstBuf> (prims_simple.h:190-330) for this member's pieces:
-  // Recv = every recv connection, Send = every send connection.
-  template <bool US, bool R, bool UD, bool S>
+  // Recv = every recv connection, Send = every send connection. The run-time fan-in and fan-out
+  // pick a compile-time instance; only reachable ones are built (R / S imply at least one
+  // connection, and Sym — the tree root's recvReduceCopySend — has as many sends as receives).
+  template <bool US, bool R, bool UD, bool S, bool Sym = false>
   __device__ __forceinline__ bool op(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
-    const int nr = R ? nRecv : 0;
-    if (nr == 0) return opS<US, 0, UD, S>(srcIx, dstIx, nelem, postOp);
-    if constexpr (MR >= 2) {
-      if (nr == 2) return opS<US, 2, UD, S>(srcIx, dstIx, nelem, postOp);
+    if constexpr (!R) {
+      return opS<US, 0, UD, S>(srcIx, dstIx, nelem, postOp);
+    } else {
+      if constexpr (MR >= 2) {
+        if (nRecv == 2) return Sym ? opN<US, 2, UD, (S ? 2 : 0)>(srcIx, dstIx, nelem, postOp)
+                                   : opS<US, 2, UD, S>(srcIx, dstIx, nelem, postOp);
+      }
+      if constexpr (MR >= 3) {
+        if (nRecv == 3) return Sym ? opN<US, 3, UD, (S ? 3 : 0)>(srcIx, dstIx, nelem, postOp)
+                                   : opS<US, 3, UD, S>(srcIx, dstIx, nelem, postOp);
+      }
+      return Sym ? opN<US, 1, UD, (S ? 1 : 0)>(srcIx, dstIx, nelem, postOp) : opS<US, 1, UD, S>(srcIx, dstIx, nelem, postOp);
     }
-    if constexpr (MR >= 3) {
-      if (nr == 3) return opS<US, 3, UD, S>(srcIx, dstIx, nelem, postOp);
-    }
-    return opS<US, 1, UD, S>(srcIx, dstIx, nelem, postOp);
   }
   template <bool US, int NR, bool UD, bool S>
   __device__ __forceinline__ bool opS(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
-    const int ns = S ? nSend : 0;
-    if (ns == 0) return opN<US, NR, UD, 0>(srcIx, dstIx, nelem, postOp);
-    if constexpr (MS >= 2) {
-      if (ns == 2) return opN<US, NR, UD, 2>(srcIx, dstIx, nelem, postOp);
+    if constexpr (!S) {
+      return opN<US, NR, UD, 0>(srcIx, dstIx, nelem, postOp);
+    } else {
+      if constexpr (MS >= 2) {
+        if (nSend == 2) return opN<US, NR, UD, 2>(srcIx, dstIx, nelem, postOp);
+      }
+      if constexpr (MS >= 3) {
+        if (nSend == 3) return opN<US, NR, UD, 3>(srcIx, dstIx, nelem, postOp);
+      }
+      return opN<US, NR, UD, 1>(srcIx, dstIx, nelem, postOp);
     }
-    if constexpr (MS >= 3) {
-      if (ns == 3) return opN<US, NR, UD, 3>(srcIx, dstIx, nelem, postOp);
-    }
-    return opN<US, NR, UD, 1>(srcIx, dstIx, nelem, postOp);
   }
   template <bool US, int NR, bool UD, int NS>
   __device__ __forceinline__ bool opN(int64_t srcIx, int64_t dstIx, int64_t nelem, bool postOp) {
@@ -489,7 +497,7 @@ __device__ __forceinline__ void tree_role(const ResParams& a, ResShared* sh, con
     const int64_t offset = off + elemOffset;
     const int64_t nelem = imin(a.chunkCount, cnt - elemOffset);
     bool ok;
-    if (t.root) ok = p.template op<true, true, true, true>(offset, offset, nelem, true);
+    if (t.root) ok = p.template op<true, true, true, true, /*Sym=*/true>(offset, offset, nelem, true);
     else if (up) ok = leaf ? p.template op<true, false, false, true>(offset, -1, nelem, false)
                            : p.template op<true, true, false, true>(offset, -1, nelem, false);
     else ok = leaf ? p.template op<false, true, true, false>(-1, offset, nelem, false)
