@@ -18,6 +18,7 @@ def test_ring_driver_under_sanitizer(tmp_path, san):
     exe = tmp_path / f"ring_stress_{san.split(',')[0]}"
     cmd = ["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={san}", "-fno-omit-frame-pointer", "-D__HIP_PLATFORM_AMD__",
            f"-I{HIP_INC}", os.path.join(ROOT, "tests", "native", "ring_stress.cpp"),
+           os.path.join(ROOT, "tests", "native", "resident_stubs.cpp"),  # the resident kernels are device code
            *[os.path.join(ROOT, "nex-nccl_amd", "csrc", f"{f}.cpp") for f in ("nexr_ring", "nexr_pat", "nexr_p2p")],
            "-x", "c", "-std=c11",
            os.path.join(ROOT, "oracle", "nexr_oracle.c"), "-x", "none",
