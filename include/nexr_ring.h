@@ -230,6 +230,14 @@ NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t comm, const void* sendbuff
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int op);
 
+/* The same all-reduce with this process's rank of the schedule inside one device-resident launch
+ * (nexrRingAllReduceResident's kernel): the ranks' launches, each in its own process, meet only
+ * through the FIFOs and the step records behind them, mapped over IPC. SIMPLE only, <= 16 ranks;
+ * every rank makes the same calls. Blocks until this rank's launch has finished; a step wait past
+ * timeoutMs returns nexrInternalError and aborts the communicator. */
+NEXR_API nexrResult_t nexrPeerRingAllReduceResident(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
+                                                    size_t count, int datatype, int op);
+
 /* The other ring collectives for this process's rank, arguments as in the thread-rank versions. */
 NEXR_API nexrResult_t nexrPeerRingReduceScatter(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
                                                 size_t recvcount, int datatype, int op);

@@ -77,6 +77,7 @@ struct Conn {
 // the rendezvous, every connection's head/tail counters and a common abort word. Slot r belongs to
 // rank r: its FIFO's IPC handle and the counters of the connection INTO rank r.
 constexpr uint32_t kPeerMagic = 0x6e657872u;  // "nexr"
+constexpr size_t kPeerResidentRecordBytes = 128 * 256;  // kResMaxTeam x kResCtrBytes (nexr_resident.h)
 struct alignas(64) PeerHeader {
   std::atomic<uint32_t> initState;  // 0 fresh, 1 being configured, 2 configured
   std::atomic<uint32_t> joined;

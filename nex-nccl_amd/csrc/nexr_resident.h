@@ -12,6 +12,7 @@ constexpr int kResMaxParts = 64;   // channel parts (MAXCHANNELS)
 constexpr int kResMaxTeam = 128;   // workgroups per (rank, channel)
 constexpr int kResCtrBytes = 256;  // one (channel, rank, team member) record: tail line + head line
 constexpr int kResHeadOff = 128;   // byte offset of the head word in a record
+static_assert((size_t)kResMaxTeam * kResCtrBytes == 128 * 256, "process ranks reserve this much behind each FIFO");
 
 // One (channel, rank) of the ring, static for the communicator. Record (ch, r, g) of a device's
 // counter block sits at ((ch * nRanks + r) * kResMaxTeam + g) * kResCtrBytes: `tail` (written by the

@@ -985,9 +985,101 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
   return r;
 }
 
+// Process ranks: this process's rank of the resident ring all-reduce. The schedule runs in one
+// launch on this rank's GPU; the other ranks' launches in their own processes meet it only through
+// the FIFOs and the step records behind them (the receiver's allocation, mapped by the sender over
+// IPC). Every rank must make the same sequence of calls.
+nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* recvbuff, size_t count, int datatype,
+                                   int op) {
+  if (!c || !c->peer) return nexrInvalidArgument;
+  if (c->proto != nexrRingProtoSimple) return nexrInvalidUsage;
+  int sem = nexrSemanticsNccl;
+  if (nexrGetSemantics(&sem) != nexrSuccess || sem == nexrSemanticsShipped) return nexrInvalidUsage;
+  size_t esz;
+  nexrDevRedOpFull red;
+  nexrResult_t r = prepare(c, datatype, op, &esz, &red);
+  if (r != nexrSuccess) return r;
+  const int n = c->cfg.nRanks, me = c->self, next = (me + 1) % n;
+  if (count > 0 && (!sendbuff || !recvbuff)) return nexrInvalidArgument;
+  if (count == 0) return nexrSuccess;
+  (void)hipSetDevice(c->devices[me]);
+  if (n == 1) return oneRank(c, me, sendbuff, recvbuff, count, datatype, red, esz);
+  if (n > nexr::kResMaxRanks) return nexrInvalidUsage;
+  int kdt = datatype;
+  if (sem == nexrSemanticsFork && red.op == nexrDevMinMax)
+    kdt = datatype == nexrInt8 ? nexrUint8 : datatype == nexrInt32 ? nexrUint32 : datatype == nexrInt64 ? nexrUint64 : datatype;
+  if (c->resDevs.empty()) {  // the (rank) table with this rank's entry, and a status word
+    c->resDevs.assign(1, c->devices[me]);
+    c->resTable.assign(1, nullptr);
+    c->resCtr.assign(1, nullptr);
+    c->resStatus.assign(1, nullptr);
+    char* fifoIn = c->conns[me]->fifo;
+    char* fifoOut = c->conns[next]->fifo;
+    std::vector<nexr::ResConn> table((size_t)n);
+    table[(size_t)me] = {fifoIn, fifoOut, fifoIn + c->cfg.buffBytes, fifoOut + c->cfg.buffBytes};
+    if (hipMalloc(&c->resTable[0], sizeof(nexr::ResConn) * table.size()) != hipSuccess ||
+        hipMemcpy(c->resTable[0], table.data(), sizeof(nexr::ResConn) * table.size(), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipHostMalloc((void**)&c->resStatus[0], sizeof(uint32_t), hipHostMallocMapped | hipHostMallocPortable) !=
+            hipSuccess) {
+      freeResident(c);
+      return nexrUnhandledCudaError;
+    }
+    *c->resStatus[0] = 0;
+  }
+  const Geom g = kGeomRing;
+  std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, 2);  // process ranks: 1 channel
+  nexr::ResParams a{};
+  a.coll = nexr::kResAllReduce;
+  a.count = (int64_t)count;
+  a.nRanks = n;
+  a.nParts = (int)parts.size();
+  for (size_t i = 0; i < parts.size(); i++) {
+    a.partOffset[i] = parts[i].offset;
+    a.partCount[i] = parts[i].count;
+    a.partChannel[i] = 0;
+  }
+  a.chunkCount = chunkElems(c, g, esz, false, 0);
+  a.stepElems = (int64_t)(c->stepBytes / esz);
+  a.stepBytes = c->stepBytes;
+  a.stepPerSlice = g.sliceSteps;
+  a.slicePerChunk = g.chunkSteps / g.sliceSteps;
+  a.redArg = red.scalarArg;
+  a.timeoutTicks = (uint64_t)(c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 100000ull;
+  a.input[me] = (const char*)sendbuff;
+  a.output[me] = (char*)recvbuff;
+  a.rankOf[0] = me;
+  a.conns = (const nexr::ResConn*)c->resTable[0];
+  a.status = c->resStatus[0];
+  // The team size must be the same on every rank (member g meets member g): it depends only on
+  // arguments all ranks share, and the occupancy cap is the same kernel on the same GPU model.
+  a.team = residentTeam(1, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
+  int perCU = 0, cus = 0;
+  if (nexr::resident_blocks_per_cu(kdt, red.op, red.scalarArg, a.coll, &perCU) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->devices[me]) != hipSuccess)
+    return nexrUnhandledCudaError;
+  if ((long)a.nParts * a.team > (long)perCU * cus) a.team = (int)((long)perCU * cus / a.nParts);
+  if (a.team < 1) return nexrInvalidUsage;
+  hipStream_t s = c->streams[me];
+  if (nexr::launch_resident(kdt, red.op, a, a.nParts * a.team, s) != hipSuccess) r = nexrUnhandledCudaError;
+  if (hipStreamSynchronize(s) != hipSuccess && r == nexrSuccess) r = nexrUnhandledCudaError;
+  if (r == nexrSuccess && __atomic_load_n(c->resStatus[0], __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
+  if (r != nexrSuccess) {
+    c->broken = true;
+    peerHeader(c->shm)->abort.store(1);
+  }
+  return r;
+}
+
 }  // namespace nexr_emu
 
 extern "C" {
+
+NEXR_API nexrResult_t nexrPeerRingAllReduceResident(nexrRingComm_t c, const void* sendbuff, void* recvbuff,
+                                                    size_t count, int datatype, int op) {
+  DeviceGuard dg(true);
+  return residentPeerAllReduce(c, sendbuff, recvbuff, count, datatype, op);
+}
 
 NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t c, const void* const* sendbuffs,
                                                 void* const* recvbuffs, size_t count, int datatype, int op) {
@@ -1341,8 +1433,14 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   // NEXR_PEER_FIFO_UNCACHED=0 selects ordinary (coarse-grained) device memory instead.
   const char* unc = getenv("NEXR_PEER_FIFO_UNCACHED");
   const bool uncached = !(unc && unc[0] == '0');
-  if ((uncached ? hipExtMallocWithFlags((void**)&c->conns[me]->fifo, c->cfg.buffBytes, hipDeviceMallocUncached)
-                : hipMalloc((void**)&c->conns[me]->fifo, c->cfg.buffBytes)) != hipSuccess)
+  // Behind the FIFO, in the same allocation (so the sender maps both with the one IPC handle): the
+  // step records of the resident all-reduce's connection into this rank, zeroed before the handle is
+  // published (nexrPeerRingAllReduceResident).
+  const size_t allocBytes = c->cfg.buffBytes + kPeerResidentRecordBytes;
+  if ((uncached ? hipExtMallocWithFlags((void**)&c->conns[me]->fifo, allocBytes, hipDeviceMallocUncached)
+                : hipMalloc((void**)&c->conns[me]->fifo, allocBytes)) != hipSuccess ||
+      hipMemset(c->conns[me]->fifo + c->cfg.buffBytes, 0, kPeerResidentRecordBytes) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
     return fail(nexrUnhandledCudaError);
   // Rendezvous segment.
   c->shmBytes = peerShmBytes(n);

@@ -22,7 +22,8 @@ RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceSc
                     "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
                     "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv",
                     "nexrRingAllReduceResident", "nexrRingReduceScatterResident", "nexrRingAllGatherResident",
-                    "nexrRingReduceResident", "nexrRingBroadcastResident", "nexrTreeAllReduceResident")
+                    "nexrRingReduceResident", "nexrRingBroadcastResident", "nexrTreeAllReduceResident",
+                    "nexrPeerRingAllReduceResident")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -68,6 +69,9 @@ def ring_lib() -> ctypes.CDLL:
         L.nexrRingAllReduceResident.restype = ctypes.c_int
         L.nexrTreeAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
         L.nexrTreeAllReduceResident.restype = ctypes.c_int
+        L.nexrPeerRingAllReduceResident.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.nexrPeerRingAllReduceResident.restype = ctypes.c_int
         _arr, _i, _sz = ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t
         for f, extra in ((L.nexrRingReduceScatterResident, [_i, _i]), (L.nexrRingAllGatherResident, [_i]),
                          (L.nexrRingReduceResident, [_i, _i, _i]), (L.nexrRingBroadcastResident, [_i, _i])):
@@ -272,6 +276,12 @@ class PeerRingComm:
     def all_reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int) -> None:
         _check(ring_lib().nexrPeerRingAllReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
                                                 int(datatype), int(op)), "nexrPeerRingAllReduce")
+
+    def all_reduce_resident(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int) -> None:
+        """This rank's part of the all-reduce as one device-resident launch (nexrPeerRingAllReduceResident)."""
+        _check(ring_lib().nexrPeerRingAllReduceResident(self._h, int(sendbuff) or None, int(recvbuff) or None,
+                                                        int(count), int(datatype), int(op)),
+               "nexrPeerRingAllReduceResident")
 
     def reduce_scatter(self, sendbuff: int, recvbuff: int, recvcount: int, datatype: int, op: int) -> None:
         _check(ring_lib().nexrPeerRingReduceScatter(self._h, int(sendbuff) or None, int(recvbuff) or None,

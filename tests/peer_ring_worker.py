@@ -24,8 +24,8 @@ def main() -> int:
     for name in ("rank", "n", "dt", "op", "count", "seed", "proto", "buff", "calls"):
         ap.add_argument(f"--{name}", type=int, required=True)
     ap.add_argument("--coll", default="allreduce",
-                    choices=["allreduce", "reducescatter", "allgather", "reduce", "broadcast", "pat_rs", "pat_ag",
-                             "sendrecv"])
+                    choices=["allreduce", "allreduce_resident", "reducescatter", "allgather", "reduce", "broadcast",
+                             "pat_rs", "pat_ag", "sendrecv"])
     ap.add_argument("--root", type=int, default=0)
     ap.add_argument("--shm", required=True)
     ap.add_argument("--out", required=True)
@@ -46,9 +46,10 @@ def main() -> int:
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
     recv = torch.zeros(n_out, dtype=send.dtype, device=dev)
     torch.cuda.synchronize()
+    resident = a.coll == "allreduce_resident"
     with ring.PeerRingComm(a.n, a.rank, a.shm, device=ordinal, buff_bytes=a.buff, protocol=a.proto,
-                           timeout_ms=60000) as comm:
-        if a.coll != "allreduce":
+                           timeout_ms=20000 if resident else 60000) as comm:
+        if a.coll not in ("allreduce", "allreduce_resident"):
             for call in range(a.calls):
                 if a.coll == "reducescatter":
                     comm.reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
@@ -70,11 +71,12 @@ def main() -> int:
                                    a.root)
                 np.save(f"{a.out}.{call}.npy", recv.cpu().numpy())
             return 0
-        comm.all_reduce(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+        all_reduce = comm.all_reduce_resident if resident else comm.all_reduce
+        all_reduce(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
         np.save(f"{a.out}.0.npy", recv.cpu().numpy())
         for call in range(1, a.calls):
             # in place on the previous result: out_c = allreduce(out_{c-1})
-            comm.all_reduce(recv.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+            all_reduce(recv.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
             np.save(f"{a.out}.{call}.npy", recv.cpu().numpy())
     return 0
 

@@ -80,6 +80,23 @@ def test_peer_ring_processes_match_fold_order(oracle, tmp_path, n, dt, op, proto
         assert mg.canon_bytes(dt, outs[r][1]) == mg.canon_bytes(dt, exp1[r]), f"rank {r}, call 1 (in place)"
 
 
+@pytest.mark.parametrize("n,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 0), (4, mg.I32, 3), (2, mg.F16, 4)])
+def test_peer_ring_resident_processes(oracle, tmp_path, n, dt, op):
+    """nexrPeerRingAllReduceResident: each process runs its rank's schedule in one device-resident
+    launch; the launches of different processes meet only through the FIFOs and the step records
+    behind them, mapped over IPC (on one GPU the ranks' kernels run side by side on it). Two calls,
+    the second in place: equal to the fold-order oracle, as the host-sequenced process ring is."""
+    from oracle.ring import ring_allreduce_expected
+    count, buff = 200_003, 1 << 18
+    outs = _run_ring(tmp_path, n, dt, op, count, 0, buff, coll="allreduce_resident")
+    inputs = mg.gen_inputs(dt, n, count, 7, special=True)
+    exp0 = ring_allreduce_expected(inputs, dt, op, buff)
+    exp1 = ring_allreduce_expected([exp0[r] for r in range(n)], dt, op, buff)
+    for r in range(n):
+        assert mg.canon_bytes(dt, outs[r][0]) == mg.canon_bytes(dt, exp0[r]), f"rank {r}, call 0"
+        assert mg.canon_bytes(dt, outs[r][1]) == mg.canon_bytes(dt, exp1[r]), f"rank {r}, call 1 (in place)"
+
+
 def test_peer_ring_c1_two_processes_fp32_sum(tmp_path):
     # BASELINE configs[0] (fp32 sum all-reduce, 4 MiB, 2 ranks) with real process ranks.
     count = 1 << 20

@@ -128,7 +128,7 @@ def resident_ring(n_ranks: int, sizes=(1 << 22, 1 << 26, 1 << 28), channels=(1, 
     return out
 
 
-PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2}
+PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2, "simple_resident": 0}  # the last: nexrPeerRingAllReduceResident
 LL_COUNT = 1 << 20  # the LL protocols run C1's 4 MiB only (they move 2x / 16/15x the payload)
 
 
@@ -146,17 +146,18 @@ def ring_rank(rank: int, n_ranks: int, shm: str, counts) -> int:
         out[pname] = res = {}
         with ring.PeerRingComm(n_ranks, rank, f"{shm}_{pname}", device=dev, protocol=proto,
                                timeout_ms=30000) as comm:
-            for count in (counts if pname == "simple" else [LL_COUNT]):
+            call = comm.all_reduce_resident if pname == "simple_resident" else comm.all_reduce
+            for count in (counts if pname.startswith("simple") else [LL_COUNT]):
                 x = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) + rank
                 y = torch.empty_like(x)
                 exp = (torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) * n_ranks
                        + n_ranks * (n_ranks - 1) // 2)
                 torch.cuda.synchronize()
-                comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)  # warm-up, connects the FIFOs
+                call(x.data_ptr(), y.data_ptr(), count, 7, 0)  # warm-up, connects the FIFOs
                 iters = 5
                 t0 = time.perf_counter()
                 for _ in range(iters):
-                    comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0)
+                    call(x.data_ptr(), y.data_ptr(), count, 7, 0)
                 dt = (time.perf_counter() - t0) / iters
                 res[str(count * 4)] = {"ms": round(dt * 1e3, 3), "algbw_GBps": round(count * 4 / dt / 1e9, 2),
                                        "exact": bool(torch.equal(y, exp))}
@@ -195,7 +196,8 @@ def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "104
     r0 = lines[0]["results"]
     exact_all = all(v["exact"] for ln in lines for proto in ln["results"].values() for v in proto.values())
     return {"per_protocol_bytes": r0, "exact_all_ranks": exact_all, "gpus": [ln["gpu"] for ln in lines],
-            "ranks": f"{n_ranks} processes, rank r on GPU r, fp32 sum; SIMPLE at 4 and 64 MiB, LL and LL128 at 4 MiB; "
+            "ranks": f"{n_ranks} processes, rank r on GPU r, fp32 sum; SIMPLE (host-sequenced and device-resident) at "
+                     "4 and 64 MiB, LL and LL128 at 4 MiB; "
                      "timings of rank 0"}
 
 
