@@ -56,7 +56,8 @@ struct ResParams {
   int64_t stepElems;         // elements per FIFO step
   uint64_t stepBytes;
   uint64_t redArg;           // op argument; also the pre-op scalar (Primitives' redOpArgs[0])
-  uint32_t* status;          // this device's status word (pinned host memory): 1 = a wait timed out
+  uint32_t* status;          // this device's status word (pinned host memory): 1 = a wait timed out,
+                             // 2 = the host aborted the call (another GPU's launch failed)
   uint64_t timeoutTicks;     // s_memrealtime ticks (100 MHz)
   int64_t count;             // ReduceScatter recvcount / AllGather sendcount (rank segment stride)
   int stepPerSlice, slicePerChunk;  // ProtoSimple<SlicePerChunk, StepPerSlice> (collectives.h:16-25)

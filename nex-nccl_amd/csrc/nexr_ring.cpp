@@ -974,6 +974,8 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
     else
       used.push_back(s);
   }
+  if (r != nexrSuccess)  // a GPU's launch failed: the ones already running would wait for its ranks
+    for (size_t d = 0; d < used.size(); d++) __atomic_store_n(c->resStatus[d], 2u, __ATOMIC_RELEASE);
   for (size_t d = 0; d < used.size(); d++) {
     (void)hipSetDevice(c->resDevs[d]);
     if (hipStreamSynchronize(used[d]) != hipSuccess)
