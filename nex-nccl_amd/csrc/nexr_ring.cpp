@@ -4,6 +4,9 @@
 // all-reduce, 4 MiB, 2 CPU-emulated ranks") and for every other caller of the primitive: the
 // schedules are unchanged, only the primitive underneath is the MI355X kernel.
 #include <fcntl.h>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -868,6 +871,27 @@ nexrResult_t ensureResidentTree(nexrRingComm* c, bool multi) {
   return nexrSuccess;
 }
 
+// Workgroups of the (datatype, op, collective) resident kernel that `device` keeps resident at once:
+// blocks per CU x CUs, queried once per process and kernel (a resident call is ~30 us; the queries
+// are host work the C1 path would otherwise repeat).
+nexrResult_t residentCapacity(int device, int kdt, int devOp, uint64_t redArg, int coll, long* capacity) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, bool, int>, long> cache;
+  const auto key = std::make_tuple(device, kdt, devOp, (redArg & 1) == 0, coll);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) {
+    *capacity = it->second;
+    return nexrSuccess;
+  }
+  int perCU = 0, cus = 0;
+  if (nexr::resident_blocks_per_cu(kdt, devOp, redArg, coll, &perCU) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return nexrUnhandledCudaError;
+  *capacity = cache[key] = (long)perCU * cus;
+  return nexrSuccess;
+}
+
 // Workgroups per (rank, channel): NEXR_RESIDENT_TEAM, else as many as give every member at least
 // 16 KiB of a full slice (StepPerSlice steps), at most about 512 workgroups on the busiest device (two
 // per CU) and at most kResMaxTeam. Measured on MI355X (tools/resident_time.py, 2 ranks, 256 MiB):
@@ -951,12 +975,10 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
   // the team shrinks to what the kernel's occupancy allows on every device used.
   long capacity = -1;
   for (size_t d = 0; d < c->resDevs.size(); d++) {
-    int perCU = 0, cus = 0;
+    long cap = 0;
     if (hipSetDevice(c->resDevs[d]) != hipSuccess ||
-        nexr::resident_blocks_per_cu(kdt, red.op, red.scalarArg, a.coll, &perCU) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->resDevs[d]) != hipSuccess)
+        residentCapacity(c->resDevs[d], kdt, red.op, red.scalarArg, a.coll, &cap) != nexrSuccess)
       return nexrUnhandledCudaError;
-    const long cap = (long)perCU * cus;
     capacity = capacity < 0 ? cap : std::min(capacity, cap);
   }
   if ((long)busiest * roles * a.nParts * a.team > capacity) a.team = (int)(capacity / ((long)busiest * roles * a.nParts));
@@ -1056,11 +1078,10 @@ nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* 
   // The team size must be the same on every rank (member g meets member g): it depends only on
   // arguments all ranks share, and the occupancy cap is the same kernel on the same GPU model.
   a.team = residentTeam(1, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
-  int perCU = 0, cus = 0;
-  if (nexr::resident_blocks_per_cu(kdt, red.op, red.scalarArg, a.coll, &perCU) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->devices[me]) != hipSuccess)
+  long capacity = 0;
+  if (residentCapacity(c->devices[me], kdt, red.op, red.scalarArg, a.coll, &capacity) != nexrSuccess)
     return nexrUnhandledCudaError;
-  if ((long)a.nParts * a.team > (long)perCU * cus) a.team = (int)((long)perCU * cus / a.nParts);
+  if ((long)a.nParts * a.team > capacity) a.team = (int)(capacity / a.nParts);
   if (a.team < 1) return nexrInvalidUsage;
   hipStream_t s = c->streams[me];
   if (nexr::launch_resident(kdt, red.op, a, a.nParts * a.team, s) != hipSuccess) r = nexrUnhandledCudaError;
