@@ -1,11 +1,12 @@
-// nexr_resident.hip — the ring collectives as ONE device-resident launch per GPU.
+// nexr_resident.hip — the ring and tree collectives as ONE device-resident launch per GPU
+// (SURVEY §8(f) #1/#4).
 //
 // What it runs is the reference's device kernel for ncclAllReduce with NCCL_ALGO_RING /
 // NCCL_PROTO_SIMPLE — runRing (src/device/all_reduce.h:12-84), and likewise ReduceScatter
-// (reduce_scatter.h:12-52), AllGather (all_gather.h:12-66), Reduce (reduce.h:12-50) and Broadcast
-// (broadcast.h:12-58) — over Primitives::genericOp
-// (src/device/prims_simple.h:190-330) with the FIFO credit protocol of waitPeer / postPeer
-// (:111-188): NCCL_STEPS = 8 slots of stepBytes per connection, a slice spans StepPerSlice steps, the
+// (reduce_scatter.h:12-52), AllGather (all_gather.h:12-66), Reduce (reduce.h:12-50), Broadcast
+// (broadcast.h:12-58) and the tree all-reduce's runTreeSplit (all_reduce.h:150-230) — over
+// Primitives::genericOp (src/device/prims_simple.h:190-330) with the FIFO credit protocol of
+// waitPeer / postPeer (:111-188): NCCL_STEPS = 8 slots of stepBytes per connection, a slice spans StepPerSlice steps, the
 // receiver waits for tail >= step + StepPerSlice, the sender for head + NCCL_STEPS >= step +
 // StepPerSlice, and each side posts its step once the slice is done. The host-sequenced ring in
 // nexr_ring.cpp runs the same schedule with one reduce-copy launch per slice; this file runs every
@@ -19,8 +20,8 @@
 //     what member g of rank r-1 produced, into bytes only they touch, so each member runs the credit
 //     protocol on its own (tail, head) record and a team needs no barrier across workgroups: the
 //     reference's one-block-per-channel FIFO, replicated `team` times over disjoint byte ranges of
-//     each slot. What every element goes through — which rank reduces it at
-//     which step, operand order, rounding — is the reference's, so results equal the host ring's.
+//     each slot. What every element goes through (which rank reduces it at which step, operand
+//     order, rounding) is the reference's, so results equal the host-sequenced schedules'.
 //   - FIFO data moves with system-coherent 16-byte buffer accesses (sc0 sc1, as the LL steps'
 //     wire accesses, nexr_ll.hip): the consumer may sit on another XCD or another GPU, whose caches
 //     do not snoop the producer's writes; with every wave's accesses drained before the one-lane
