@@ -60,6 +60,7 @@ CONFIGS = {
 EXTRA_ORDER = ["c3_f16", "c3_bf16", "c4_i32_min", "c4_i32_max", "c4_i32_prod", "c4_i8_min", "c4_i8_max",
                "c4_i8_prod"]
 ESZ = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2}
+FANOUT_SETS = 3  # rotating buffer sets per GPU, in every leg (N = 1 line, torchrun ranks, fan-out)
 METRIC = "device-resident reduce-copy GB/s, fp32 sum, K-way fan-in, 1/2/4/8 MI355X"
 KERNEL = "nexr::reduce_copy_kernel"
 DATA = "synthetic (uniform [-1,1) generated on device; inputs resident in HBM)"
@@ -209,6 +210,64 @@ class DeviceWorkload:
         sp, dp, _, _ = self.sets[i % len(self.sets)]
         return self.pkg.make_work(sp, dp, self.n, self.cfg["arg"])
 
+    def per_set(self, rounds: int = 6) -> dict:
+        """After the timed region: `rounds` x sets more launches, round-robin over the sets as in the
+        timed loop, with HIP events around every launch on the launch stream; the average kernel
+        time of each set and where its buffers sit (the same kernel ran one set of C3 at
+        0.81-0.83 of peak and the other two at 0.75-0.77)."""
+        import torch
+        cfg, ns = self.cfg, len(self.sets)
+        evs = []
+        with torch.cuda.device(self.dev):
+            for i in range(rounds * ns):
+                sp, dp, _, _ = self.sets[i % ns]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
+                self.pkg.reduce_copy_ptrs(sp, dp, self.n, cfg["dt"], cfg["op"], cfg["arg"], None, False, self.handle)
+                e1.record(self.stream)
+                evs.append((i % ns, e0, e1))
+            torch.cuda.synchronize(self.dev)
+        us = [[] for _ in range(ns)]
+        for k, e0, e1 in evs:
+            us[k].append(e0.elapsed_time(e1) * 1e3)
+        lo = min(p for sp, dp, _, _ in self.sets for p in sp + dp)
+        return {"per_set_us": [round(sum(u) / len(u), 2) for u in us],
+                "per_set_frac": [round(algorithmic_bytes(cfg) / (sum(u) / len(u)) / 1e3 / PEAK_HBM_GBS, 4) for u in us],
+                "per_set_launches": rounds,
+                "per_set_buffers_mib": [[round((p - lo) / (1 << 20), 3) for p in sp + dp] for sp, dp, _, _ in self.sets]}
+
+    def check_exact(self, i: int, blocks: int = 256, block: int = 4096) -> dict:
+        """Test infrastructure, outside every timed region: the output of set `i` (every set holds the
+        output of its last launch; the inputs never change) against the CPU oracle, bit for bit, on a
+        strided sample of whole runs of elements (`blocks` runs of `block` spread over the buffer, plus
+        the first and the last run: >= 1 Mi elements), or on all of it when it is smaller."""
+        import numpy as np
+        import torch
+        import oracle
+        cfg, n, esz = self.cfg, self.n, ESZ[self.cfg["dt"]]
+        _, _, srcs, dsts = self.sets[i % len(self.sets)]
+        if n <= block * (blocks + 2):
+            starts = [0]
+            block = n
+        else:
+            starts = sorted({0, n - block} | {int(x) for x in np.linspace(0, n - block, blocks)})
+
+        def sample(t):
+            b = t.view(torch.uint8)
+            return torch.cat([b[s * esz:(s + block) * esz] for s in starts]).cpu().numpy()
+
+        on_gpu = self.dev.type == "cuda"
+        with torch.cuda.device(self.dev) if on_gpu else contextlib.nullcontext():
+            if on_gpu:
+                torch.cuda.synchronize(self.dev)
+            got = [sample(d) for d in dsts]
+            ins = [sample(s) for s in srcs]
+        exp = oracle.reduce_copy(ins, cfg["m"], cfg["dt"], cfg["op"], cfg["arg"])
+        ok = all(np.array_equal(g, e.view(np.uint8)) for g, e in zip(got, exp))
+        return {"exact": bool(ok), "checked_elements": len(starts) * block, "checked_set": i % len(self.sets),
+                "check": "bit-exact vs the C oracle (oracle/nexr_oracle.c) on a strided sample of the last "
+                         "launch's output, after the timed region"}
+
     def run(self, steps: int, warmup: int, dist, per_launch: bool = False):
         """Returns (local wall s, max-over-ranks wall s, average kernel s from HIP events recorded on
         the launch stream around the timed region, or around every launch)."""
@@ -232,6 +291,7 @@ class DeviceWorkload:
             kernel_s = sum(ms) / len(ms) / 1e3
         else:
             kernel_s = ev[warmup][0].elapsed_time(ev[total - 1][1]) / steps / 1e3
+        self.last_set = (total - 1) % len(self.sets)
         return local_s, max_s, kernel_s
 
     def free(self):
@@ -270,12 +330,15 @@ def extra_configs(pkg, steps: int = 20, warmup: int = 5, names=EXTRA_ORDER) -> d
         cfg = CONFIGS[name]
         wl = DeviceWorkload(pkg, cfg, local_device_index(), seed=2000 + i)
         _, _, kernel_s = wl.run(steps, warmup, _Solo())
+        sets = side_leg(wl.per_set)
+        exact = side_leg(wl.check_exact, wl.last_set)
         wl.free()
         r = roofline(cfg, name, kernel_s)
         out[name] = {"workload": cfg["workload"], "dtype": cfg["dtype"], "bytes_per_launch": algorithmic_bytes(cfg),
                      "achieved": r["achieved"], "frac": r["frac"], "avg_kernel_us": r["avg_kernel_us"],
                      "traffic": r["traffic"], "traffic_source": r["traffic_source"], "steps": steps,
-                     "warmup": warmup}
+                     "warmup": warmup, "exact": exact.get("exact"), "exact_check": exact}
+        out[name].update(sets if "error" not in sets else {"per_set_error": sets})
     return out
 
 
@@ -528,18 +591,63 @@ def _bounded(cmd, timeout_s: float):
         return {"error": repr(e)[:300]}
 
 
-def xgmi_probe(timeout_s: float = 120.0):
-    """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, in bounded
-    subprocesses: GPU 0's kernel with an operand in GPU 1's HBM and the two-rank process ring; with
-    three or more GPUs also the process ring over all of them (up to 8). Reported, never allowed to
-    fail the bench line."""
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (MI355X_MICROARCH.md; 7 links per GPU)
+
+
+def xgmi_link_rates(res: dict) -> dict:
+    """Next to every exact check of the probe, the rate that crossed xGMI against the one-link bound:
+    the peer step's remote read / write (one 256 MiB operand over the link per launch), and the ring
+    all-reduces (each rank sends 2(n-1)/n of its bytes to its successor over one link: busbw)."""
+    if not isinstance(res, dict):
+        return res
+    for key in ("remote_read", "remote_write"):
+        v = res.get(key)
+        if isinstance(v, dict) and "xgmi_GBps" in v:
+            v["link_bound_GBps"] = XGMI_LINK_GBS
+            v["frac_of_link"] = round(v["xgmi_GBps"] / XGMI_LINK_GBS, 4)
+    for key in ("ring_processes", "ring_processes_all_gpus"):
+        v = res.get(key)
+        if not isinstance(v, dict) or "per_protocol_bytes" not in v:
+            continue
+        n = len(v.get("gpus", [])) or 2
+        for proto in v["per_protocol_bytes"].values():
+            for r in proto.values():
+                if isinstance(r, dict) and "algbw_GBps" in r:
+                    r["busbw_GBps"] = round(r["algbw_GBps"] * 2 * (n - 1) / n, 2)
+                    r["frac_of_link"] = round(r["busbw_GBps"] / XGMI_LINK_GBS, 4)
+    v = res.get("resident_ring")
+    if isinstance(v, dict):
+        for r in v.values():
+            if isinstance(r, dict) and "busbw_GBps" in r:
+                r["frac_of_link"] = round(r["busbw_GBps"] / XGMI_LINK_GBS, 4)
+    res["link_bound_GBps"] = XGMI_LINK_GBS
+    return res
+
+
+def xgmi_probe(budget_s: float = 240.0):
+    """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, each part in a
+    bounded subprocess of its own so one hang cannot cost the others or the line: GPU 0's kernel with
+    an operand in GPU 1's HBM, the two-rank process ring, the resident ring over all GPUs, and with
+    three or more GPUs the process ring over all of them (up to 8). The parts share `budget_s`; a part
+    that times out is recorded as such. Reported, never allowed to fail the bench line."""
     import torch
     probe = os.path.join(ROOT, "tools", "xgmi_probe.py")
-    res = _bounded([sys.executable, probe], timeout_s)
+    t_end = time.perf_counter() + budget_s
     n_dev = torch.cuda.device_count()
-    if n_dev >= 3 and isinstance(res, dict) and "skipped" not in res:
-        res["ring_processes_all_gpus"] = _bounded([sys.executable, probe, "--ring-all", str(min(n_dev, 8))], 100.0)
-    return res
+
+    def part(args, limit):
+        left = t_end - time.perf_counter()
+        if left < 5:
+            return {"error": "skipped: the probe budget is spent"}
+        return _bounded([sys.executable, probe] + args, min(limit, left))
+
+    res = part(["--peer-step"], 60.0)
+    if isinstance(res, dict) and "skipped" not in res:
+        res["ring_processes"] = part(["--ring-only"], 75.0)
+        res["resident_ring"] = part(["--resident-only", str(min(n_dev, 8))], 60.0)
+        if n_dev >= 3:
+            res["ring_processes_all_gpus"] = part(["--ring-all", str(min(n_dev, 8))], 100.0)
+    return xgmi_link_rates(res)
 
 
 def h2d_inclusive(pkg, cfg, reps: int = 3):
@@ -648,6 +756,10 @@ def main_ranks(args, cfg, pkg) -> dict | None:
     bytes_step = algorithmic_bytes(cfg)
     value = dist.world * bytes_step * args.steps / max_s / 1e9
     ranks = dist.gather([local_s, kernel_s], wl.dev)
+    sets = exact = None
+    if dist.rank == 0:  # after the timed region: per-set times and the bit-exact check of the last output
+        sets = side_leg(wl.per_set)
+        exact = side_leg(wl.check_exact, wl.last_set)
     c5 = None
     if dist.world > 1:
         # Same-run legs: rank 0's GPU alone (the N=1 reference), then every GPU alone in turn.
@@ -670,6 +782,9 @@ def main_ranks(args, cfg, pkg) -> dict | None:
                            (f"; REHEARSAL: {dist.world} ranks folded onto {torch.cuda.device_count()} GPU(s)"
                             if torch.cuda.device_count() < dist.world else ""))
         result["roofline"] = roofline(cfg, args.config, kernel_s, per_launch)
+        result["roofline"].update(sets if "error" not in sets else {"per_set_error": sets})
+        result["exact"] = exact.get("exact")
+        result["exact_check"] = exact
         result["cpu_baseline"] = None
         result["h2d_inclusive"] = None
         if dist.world == 1:
@@ -707,22 +822,24 @@ def main_fanout(args, cfg, pkg) -> dict:
     if n_vis < args.gpus and not fold:
         raise SystemExit(f"--gpus {args.gpus} but only {n_vis} visible GPU(s)")
     devices = [d % n_vis for d in range(args.gpus)]
-    wls = [DeviceWorkload(pkg, cfg, dev, seed=1000 + d, sets=1) for d, dev in enumerate(devices)]
+    # Three rotating buffer sets per GPU, as the N=1 line: launch k of a GPU runs set k mod 3
+    # (nexrReduceCopyMultiDeviceSets), so no launch re-reads the previous one's cache-resident bytes.
+    wls = [DeviceWorkload(pkg, cfg, dev, seed=1000 + d, sets=FANOUT_SETS) for d, dev in enumerate(devices)]
     for d in sorted(set(devices)):
         torch.cuda.synchronize(d)
-    works = [wl.work(0) for wl in wls]
+    works = [[wl.work(s) for s in range(FANOUT_SETS)] for wl in wls]
     bytes_step = algorithmic_bytes(cfg)
 
     def timed(ws, ds):
-        pkg.reduce_copy_multi_device(ws, ds, cfg["dt"], cfg["op"], reps=max(1, args.warmup))
-        return pkg.reduce_copy_multi_device(ws, ds, cfg["dt"], cfg["op"], reps=args.steps)
+        pkg.reduce_copy_multi_device_sets(ws, ds, cfg["dt"], cfg["op"], reps=max(1, args.warmup))
+        return pkg.reduce_copy_multi_device_sets(ws, ds, cfg["dt"], cfg["op"], reps=args.steps)
 
     agg_s = timed(works, devices)
     solo = [timed([works[i]], [devices[i]]) for i in range(args.gpus)]
     value = args.gpus * bytes_step * args.steps / agg_s / 1e9
     result = base_line(cfg, args.gpus, args.steps, args.warmup, value, agg_s,
                        f"independent chunks x{args.gpus} (no collective), one process, "
-                       f"nexrReduceCopyMultiDevice (a host thread + stream per GPU)" +
+                       f"nexrReduceCopyMultiDeviceSets (a host thread + stream per GPU, {FANOUT_SETS} rotating sets)" +
                        (f"; REHEARSAL: {args.gpus} chunks folded onto {n_vis} GPU(s)" if n_vis < args.gpus else ""))
     # Roofline of the kernel itself: HIP events on GPU 0's launch stream, 3 rotating sets.
     for wl in wls:
@@ -734,7 +851,9 @@ def main_fanout(args, cfg, pkg) -> dict:
     result["cpu_baseline"] = None
     result["h2d_inclusive"] = None
     result["c5"] = c5_summary(args.gpus, bytes_step, args.steps, agg_s, solo[0], solo)
-    result["c5"]["timing"] = "nexrReduceCopyMultiDevice: barrier release to the last GPU's completion"
+    result["c5"]["timing"] = ("nexrReduceCopyMultiDeviceSets: barrier release to the last GPU's completion, "
+                              f"{FANOUT_SETS} rotating buffer sets per GPU (as the N=1 line)")
+    result["c5"]["sets_per_gpu"] = FANOUT_SETS
     if not args.no_xgmi:
         result["xgmi_probe"] = xgmi_probe()
     print(json.dumps(result), flush=True)

@@ -173,6 +173,17 @@ NEXR_API nexrResult_t nexrReduceCopyMultiDevice(const nexrReduceCopyWork* works,
                                                 int datatype, int devRedOp, int reps, double* seconds);
 
 /*
+ * nexrReduceCopyMultiDeviceSets — nexrReduceCopyMultiDevice with nSets rotating works per thread:
+ * works[i * nSets + s] (s < nSets) all run on devices[i], and launch k (k < reps) of thread i is
+ * work i * nSets + k mod nSets. With nSets buffer sets per GPU, consecutive launches never re-read
+ * the previous launch's cache-resident bytes (the N = 1 bench's rotation, applied to C5). nSets = 1
+ * is nexrReduceCopyMultiDevice. Validation, threads, streams, barrier and timing as above.
+ */
+#define NEXR_MAX_MULTI_DEVICE_SETS 8
+NEXR_API nexrResult_t nexrReduceCopyMultiDeviceSets(const nexrReduceCopyWork* works, const int* devices, int nWorks,
+                                                    int nSets, int datatype, int devRedOp, int reps, double* seconds);
+
+/*
  * nexrReduceCopyHost — the same reduce-copy for buffers in HOST memory (the emulated
  * transport's staging FIFOs, reference src/include/device.h:753-771): copies the K inputs
  * host->device, runs nexrReduceCopy, copies the M outputs device->host, and synchronises the

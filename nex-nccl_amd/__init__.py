@@ -83,7 +83,8 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
              DataType.Float8e5m2: 1}
 
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
-ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
+ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyMultiDeviceSets",
+               "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
                "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrQueryLaunch", "nexrGetPoolStats", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion",
                "nexrGetLastHipError", "nexrSetSemantics", "nexrGetSemantics")
 
@@ -165,6 +166,8 @@ def lib() -> ctypes.CDLL:
     L.nexrReduceCopyBatch.restype = i32
     L.nexrReduceCopyMultiDevice.argtypes = [P(ReduceCopyWork), P(i32), i32, i32, i32, i32, P(ctypes.c_double)]
     L.nexrReduceCopyMultiDevice.restype = i32
+    L.nexrReduceCopyMultiDeviceSets.argtypes = [P(ReduceCopyWork), P(i32), i32, i32, i32, i32, i32, P(ctypes.c_double)]
+    L.nexrReduceCopyMultiDeviceSets.restype = i32
     L.nexrHostToDevRedOp.argtypes = [P(DevRedOpFull), i32, i32, i32]
     L.nexrHostToDevRedOp.restype = i32
     L.nexrLaunchOneRank.argtypes = [vp, vp, sz, DevRedOpFull, i32, vp]
@@ -275,6 +278,25 @@ def reduce_copy_multi_device(works: Sequence[ReduceCopyWork], devices: Sequence[
     secs = ctypes.c_double(0.0)
     _check(lib().nexrReduceCopyMultiDevice(arr, dev, len(works), int(datatype), int(dev_red_op), int(reps),
                                            ctypes.byref(secs)), "nexrReduceCopyMultiDevice")
+    return secs.value
+
+
+def reduce_copy_multi_device_sets(works_per_device: Sequence[Sequence[ReduceCopyWork]], devices: Sequence[int],
+                                  datatype: int, dev_red_op: int, reps: int = 1) -> float:
+    """``nexrReduceCopyMultiDeviceSets``: ``works_per_device[i]`` (the same number of works for every
+    entry) are rotating sets on GPU devices[i]: launch k of its thread runs set k mod len. Returns
+    seconds from the start barrier to the last device's completion."""
+    if len(works_per_device) != len(devices) or not works_per_device:
+        raise NexrError(Result.InvalidArgument, "one list of works per device")
+    n_sets = len(works_per_device[0])
+    if any(len(w) != n_sets for w in works_per_device):
+        raise NexrError(Result.InvalidArgument, "the same number of sets on every device")
+    flat = [w for ws in works_per_device for w in ws]
+    arr = (ReduceCopyWork * max(1, len(flat)))(*flat)
+    dev = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+    secs = ctypes.c_double(0.0)
+    _check(lib().nexrReduceCopyMultiDeviceSets(arr, dev, len(devices), n_sets, int(datatype), int(dev_red_op),
+                                               int(reps), ctypes.byref(secs)), "nexrReduceCopyMultiDeviceSets")
     return secs.value
 
 

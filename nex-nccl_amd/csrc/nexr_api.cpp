@@ -380,11 +380,14 @@ void mdStreamGive(int dev, hipStream_t st) {  // st was synchronised without err
   std::lock_guard<std::mutex> g(gMdStreamMu);
   gMdStreamIdle.emplace_back(dev, st);
 }
-nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks, int datatype,
-                                   int op, int reps, double* seconds) {
+// nSets works per thread (works[i * nSets + s], all on devices[i]): launch k of thread i runs set
+// k mod nSets, the rotation the N = 1 bench uses so no launch re-reads cache-resident bytes.
+nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks, int nSets,
+                                   int datatype, int op, int reps, double* seconds) {
   if (nWorks < 0 || nWorks > NEXR_MAX_MULTI_DEVICE_WORKS || reps < 1) return nexrInvalidArgument;
+  if (nSets < 1 || nSets > NEXR_MAX_MULTI_DEVICE_SETS) return nexrInvalidArgument;
   if (nWorks > 0 && (works == nullptr || devices == nullptr)) return nexrInvalidArgument;
-  for (int i = 0; i < nWorks; i++) {
+  for (int i = 0; i < nWorks * nSets; i++) {
     const nexrReduceCopyWork& w = works[i];
     nexrResult_t r = validate(w.nSrcs, w.srcs, w.nDsts, w.dsts, w.nElts, datatype, op, w.redOpArg, w.nPreOpSrcs,
                               w.preOpArgs);
@@ -406,7 +409,6 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
   std::vector<int> hipErr(nWorks, 0);
   bool cancel = false;  // set (under mu) when not every work got a thread: nothing runs
   auto run = [&](int i) {
-    const nexrReduceCopyWork& w = works[i];
     hipStream_t st = nullptr;
     hipError_t e = hipSetDevice(devices[i]);
     if (e == hipSuccess) e = mdStreamTake(devices[i], &st);
@@ -424,9 +426,11 @@ nexrResult_t reduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* d
       }
       if (cancel && res[i] == nexrSuccess) res[i] = nexrSystemError;
     }
-    for (int k = 0; k < reps && res[i] == nexrSuccess; k++)
+    for (int k = 0; k < reps && res[i] == nexrSuccess; k++) {
+      const nexrReduceCopyWork& w = works[(size_t)i * nSets + k % nSets];
       res[i] = reduceCopyDevice(w.nSrcs, w.srcs, w.nDsts, w.dsts, w.nElts, datatype, op, w.redOpArg, w.nPreOpSrcs,
                                 w.preOpArgs, nullptr, w.postOp, st);
+    }
     if (res[i] == nexrUnhandledCudaError && hipErr[i] == 0) hipErr[i] = tLastHipError;
     if (st) {
       e = hipStreamSynchronize(st);
@@ -905,7 +909,11 @@ NEXR_API nexrResult_t nexrReduceCopyBatch(const nexrReduceCopyWork* works, int n
 
 NEXR_API nexrResult_t nexrReduceCopyMultiDevice(const nexrReduceCopyWork* works, const int* devices, int nWorks,
                                                 int datatype, int devRedOp, int reps, double* seconds) {
-  return reduceCopyMultiDevice(works, devices, nWorks, datatype, devRedOp, reps, seconds);
+  return reduceCopyMultiDevice(works, devices, nWorks, 1, datatype, devRedOp, reps, seconds);
+}
+NEXR_API nexrResult_t nexrReduceCopyMultiDeviceSets(const nexrReduceCopyWork* works, const int* devices, int nWorks,
+                                                    int nSets, int datatype, int devRedOp, int reps, double* seconds) {
+  return reduceCopyMultiDevice(works, devices, nWorks, nSets, datatype, devRedOp, reps, seconds);
 }
 
 NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,

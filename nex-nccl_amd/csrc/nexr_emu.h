@@ -92,6 +92,14 @@ struct PeerSlot {
   hipIpcMemHandle_t fifoHandle;
   std::atomic<uint32_t> claimed;  // set once by rank r when it joins; already set = stale segment
   alignas(64) ConnState conn;
+  // Resident all-reduces rank r has completed (nexrPeerRingAllReduceResident): its kernel no longer
+  // reads its receive FIFO. The ring link's two users hand over through this and conn (ringLinkHandover).
+  alignas(64) std::atomic<uint64_t> residentDone;
+  // Rank r's first resident call publishes its GPU (PCI domain/bus/device) and the team its GPU can
+  // keep resident; every rank then runs the minimum (member g only meets member g of its neighbours).
+  std::atomic<uint64_t> residentGpu;
+  std::atomic<int64_t> residentCap;   // workgroups per part rank r's GPU keeps resident
+  std::atomic<int32_t> residentTeam;  // rank r's proposed team; 0 = not published yet
 };
 // Links beyond the ring for PAT (r -> r +- 2^d) and P2P (any r -> q), one per ordered pair: the
 // receiver's FIFO handles and the link's counters. Only for communicators of up to kPeerLinkMaxRanks.
@@ -164,6 +172,9 @@ struct nexrRingComm {
   std::vector<uint32_t*> resStatus;
   // Process ranks: this process is rank `self` only.
   bool peer = false;
+  int ringLinkUser = 0;          // last user of the ring link r -> r+1: 0 none, 1 host-sequenced, 2 resident
+  uint64_t residentCalls = 0;    // resident all-reduces this rank has completed
+  int residentTeamAgreed = 0;    // process ranks: the team size all ranks agreed on (first resident call)
   int self = 0;
   void* shm = nullptr;
   size_t shmBytes = 0;
@@ -420,5 +431,6 @@ nexrResult_t ensureSecondStreams(nexrRingComm* c);
 // Process ranks: connect this rank's PAT (p2p = false) or P2P links on first use (collective).
 nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p);
 nexrResult_t peerFinish(nexrRingComm* c, Shared& sh);
+nexrResult_t ringLinkHandover(nexrRingComm* c, bool resident);
 
 }  // namespace nexr_emu

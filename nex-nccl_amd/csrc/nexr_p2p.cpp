@@ -160,8 +160,12 @@ NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t c, const void* sendbuff, i
     return peerFinish(c, sh);
   }
   std::thread sender;
-  if (sendPeer >= 0) sender = std::thread([&] { runP2pHalf(c, &sh, me, true, sendPeer, sendbuff, recvbuff, bytes); });
-  if (recvPeer >= 0) runP2pHalf(c, &sh, me, false, recvPeer, sendbuff, recvbuff, bytes);
+  try {
+    if (sendPeer >= 0) sender = std::thread([&] { runP2pHalf(c, &sh, me, true, sendPeer, sendbuff, recvbuff, bytes); });
+  } catch (...) {
+    sh.fail(nexrSystemError);  // no send half: the peers see the abort word, this rank's recv is skipped
+  }
+  if (recvPeer >= 0 && !sh.aborted()) runP2pHalf(c, &sh, me, false, recvPeer, sendbuff, recvbuff, bytes);
   if (sender.joinable()) sender.join();
   return peerFinish(c, sh);
 }

@@ -679,6 +679,8 @@ nexrResult_t peerPat(nexrRingComm* c, bool reduceScatter, const void* sendbuff, 
     if (c->shm) peerHeader(c->shm)->abort.store(1);
     return r;
   }
+  r = ringLinkHandover(c, false);  // PAT's r -> r+1 link is the ring's
+  if (r != nexrSuccess) return r;
   Shared sh;
   sh.remoteAbort = &peerHeader(c->shm)->abort;
   const ChannelPart part{0, 0, (int64_t)count, patChunkElems(c, esz, !reduceScatter, (int64_t)count)};

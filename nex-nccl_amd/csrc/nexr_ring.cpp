@@ -6,6 +6,7 @@
 #include <fcntl.h>
 #include <map>
 #include <mutex>
+#include <system_error>
 #include <tuple>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -378,11 +379,29 @@ nexrResult_t prepare(nexrRingComm* c, int datatype, int op, size_t* esz, nexrDev
   return nexrHostToDevRedOp(red, op, datatype, c->cfg.nRanks);
 }
 
+// Test hook: NEXR_TEST_SPAWN_FAIL_AT=k makes the k-th thread creation (1-based) of the next
+// runThreads calls throw, as std::thread does when the system is out of threads.
+static void spawnHook(size_t k) {
+  const char* e = getenv("NEXR_TEST_SPAWN_FAIL_AT");
+  if (e && *e && (size_t)strtoull(e, nullptr, 10) == k)
+    throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again), "spawn hook");
+}
+
 // Runs `jobs` (one per emulated rank, or per tree half) on host threads and collects the first error.
+// If a thread cannot be created, the ones already running are told to give up (their spins see the
+// abort), joined, and the call reports nexrSystemError with the communicator broken: nothing throws
+// through the C entry points and no joinable thread is ever destroyed.
 nexrResult_t runThreads(nexrRingComm* c, Shared& sh, const std::vector<std::function<void()>>& jobs) {
   std::vector<std::thread> threads;
-  threads.reserve(jobs.size());
-  for (const auto& j : jobs) threads.emplace_back(j);
+  try {
+    threads.reserve(jobs.size());
+    for (const auto& j : jobs) {
+      spawnHook(threads.size() + 1);
+      threads.emplace_back(j);
+    }
+  } catch (...) {
+    sh.fail(nexrSystemError);
+  }
   for (auto& t : threads) t.join();
   if (sh.firstError.load() != 0) {
     c->broken = true;  // step counters are mid-protocol: the communicator cannot be reused
@@ -568,6 +587,8 @@ nexrResult_t peerCollective(nexrRingComm* c, RingColl coll, const void* sendbuff
   if (count == 0) return nexrSuccess;
   (void)hipSetDevice(c->devices[me]);
   if (n == 1) return oneRank(c, me, sendbuff, recvbuff, count, datatype, red, esz);
+  r = ringLinkHandover(c, false);
+  if (r != nexrSuccess) return r;
   Shared sh;
   sh.remoteAbort = &peerHeader(c->shm)->abort;
   const Geom g = (coll == kReduce || coll == kBroadcast) ? kGeomPipe : kGeomRing;
@@ -667,6 +688,37 @@ nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
     }
   }
   return nexrSuccess;
+}
+
+// Process ranks: the ring link r -> r+1 (rank r+1's receive FIFO) serves two users with separate
+// step counters: the host-sequenced collectives (head/tail in the shared segment, also PAT's ring
+// link) and the resident all-reduce (records behind the FIFO). Either returns once this rank's own
+// schedule is done, while rank r+1 may still be reading the last slots it was sent. Before this
+// rank writes the link as the other user, it waits until rank r+1 has consumed everything the
+// previous user sent: head == tail after host-sequenced calls, or rank r+1's kernel done after
+// resident ones. Bounded by the communicator's timeout and its abort word, as every other wait.
+nexrResult_t ringLinkHandover(nexrRingComm* c, bool resident) {
+  const int want = resident ? 2 : 1;
+  const int prev = c->ringLinkUser;
+  c->ringLinkUser = want;
+  if (prev == 0 || prev == want) return nexrSuccess;
+  const int n = c->cfg.nRanks, next = (c->self + 1) % n;
+  PeerSlot* s = peerSlot(c->shm, next);
+  PeerHeader* h = peerHeader(c->shm);
+  const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const bool drained = resident
+                             ? s->conn.head.load(std::memory_order_acquire) >= s->conn.tail.load(std::memory_order_acquire)
+                             : s->residentDone.load(std::memory_order_acquire) >= c->residentCalls;
+    if (drained) return nexrSuccess;
+    if (h->abort.load(std::memory_order_acquire)) break;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) break;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  c->broken = true;
+  h->abort.store(1);
+  return nexrRemoteError;
 }
 
 nexrResult_t peerFinish(nexrRingComm* c, Shared& sh) {
@@ -1009,6 +1061,52 @@ nexrResult_t residentCollective(nexrRingComm* c, RingColl coll, const void* cons
   return r;
 }
 
+// Process ranks, first resident call: publish this rank's GPU and its proposed team (`want`, capped
+// by what its GPU keeps resident, `perPartCap` workgroups per part), wait for every rank, then run
+// min over ranks of min(want, perPartCap / ranks sharing that GPU): every rank launches the same
+// team, and the grids of ranks that share a GPU fit on it together. Collective, bounded by the
+// communicator's timeout and abort word.
+nexrResult_t residentPeerTeam(nexrRingComm* c, int want, long perPartCap) {
+  const int n = c->cfg.nRanks, me = c->self;
+  int dom = 0, bus = 0, dev = 0;
+  if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->devices[me]) != hipSuccess ||
+      hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->devices[me]) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, c->devices[me]) != hipSuccess)
+    return nexrUnhandledCudaError;
+  PeerSlot* mine = peerSlot(c->shm, me);
+  mine->residentGpu.store(((uint64_t)(uint32_t)dom << 32) | ((uint64_t)(bus & 0xffff) << 16) | (uint64_t)(dev & 0xffff),
+                          std::memory_order_relaxed);
+  mine->residentCap.store(perPartCap, std::memory_order_relaxed);
+  mine->residentTeam.store(std::max(1, want), std::memory_order_release);
+  PeerHeader* h = peerHeader(c->shm);
+  const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < n; r++) {
+    while (peerSlot(c->shm, r)->residentTeam.load(std::memory_order_acquire) == 0) {
+      if (h->abort.load(std::memory_order_acquire) ||
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) {
+        c->broken = true;
+        h->abort.store(1);
+        return nexrRemoteError;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+  // Every rank evaluates the same expression over the same published values.
+  long team = nexr::kResMaxTeam;
+  for (int r = 0; r < n; r++) {
+    const PeerSlot* sr = peerSlot(c->shm, r);
+    const uint64_t gpu = sr->residentGpu.load(std::memory_order_relaxed);
+    int sharing = 0;
+    for (int q = 0; q < n; q++) sharing += peerSlot(c->shm, q)->residentGpu.load(std::memory_order_relaxed) == gpu;
+    team = std::min<long>(team, sr->residentTeam.load(std::memory_order_relaxed));
+    team = std::min<long>(team, sr->residentCap.load(std::memory_order_relaxed) / std::max(1, sharing));
+  }
+  if (team < 1) return nexrInvalidUsage;
+  c->residentTeamAgreed = (int)std::min<long>(team, nexr::kResMaxTeam);
+  return nexrSuccess;
+}
+
 // Process ranks: this process's rank of the resident ring all-reduce. The schedule runs in one
 // launch on this rank's GPU; the other ranks' launches in their own processes meet it only through
 // the FIFOs and the step records behind them (the receiver's allocation, mapped by the sender over
@@ -1075,22 +1173,47 @@ nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* 
   a.rankOf[0] = me;
   a.conns = (const nexr::ResConn*)c->resTable[0];
   a.status = c->resStatus[0];
-  // The team size must be the same on every rank (member g meets member g): it depends only on
-  // arguments all ranks share, and the occupancy cap is the same kernel on the same GPU model.
-  a.team = residentTeam(1, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
-  long capacity = 0;
-  if (residentCapacity(c->devices[me], kdt, red.op, red.scalarArg, a.coll, &capacity) != nexrSuccess)
-    return nexrUnhandledCudaError;
-  if ((long)a.nParts * a.team > capacity) a.team = (int)(capacity / a.nParts);
-  if (a.team < 1) return nexrInvalidUsage;
+  // The team size must be the same on every rank (member g meets member g), and every rank's grid
+  // must stay resident beside the other ranks' grids on the same GPU: agreed once, through the
+  // shared segment (residentPeerTeam).
+  if (c->residentTeamAgreed == 0) {
+    int team = residentTeam(1, a.nParts, c->stepBytes * (size_t)a.stepPerSlice);
+    long capacity = 0;
+    if (residentCapacity(c->devices[me], kdt, red.op, red.scalarArg, a.coll, &capacity) != nexrSuccess)
+      return nexrUnhandledCudaError;
+    r = residentPeerTeam(c, team, capacity / a.nParts);
+    if (r != nexrSuccess) return r;
+  }
+  a.team = c->residentTeamAgreed;
+  r = ringLinkHandover(c, true);
+  if (r != nexrSuccess) return r;
   hipStream_t s = c->streams[me];
   if (nexr::launch_resident(kdt, red.op, a, a.nParts * a.team, s) != hipSuccess) r = nexrUnhandledCudaError;
+  // Wait for the kernel while relaying the communicator's abort word (set by a failing rank in another
+  // process) into this GPU's status word, which the kernel's waits poll: a rank's failure then ends
+  // every rank's kernel at once instead of after the full timeout.
+  PeerHeader* ph = peerHeader(c->shm);
+  for (bool relayed = false; r == nexrSuccess;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) {
+      r = nexrUnhandledCudaError;
+      break;
+    }
+    if (!relayed && ph->abort.load(std::memory_order_acquire)) {
+      __atomic_store_n(c->resStatus[0], 2u, __ATOMIC_RELEASE);
+      relayed = true;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(5));
+  }
   if (hipStreamSynchronize(s) != hipSuccess && r == nexrSuccess) r = nexrUnhandledCudaError;
   if (r == nexrSuccess && __atomic_load_n(c->resStatus[0], __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
   if (r != nexrSuccess) {
     c->broken = true;
     peerHeader(c->shm)->abort.store(1);
+    return r;
   }
+  peerSlot(c->shm, me)->residentDone.store(++c->residentCalls, std::memory_order_release);
   return r;
 }
 

@@ -24,7 +24,7 @@ def main() -> int:
     for name in ("rank", "n", "dt", "op", "count", "seed", "proto", "buff", "calls"):
         ap.add_argument(f"--{name}", type=int, required=True)
     ap.add_argument("--coll", default="allreduce",
-                    choices=["allreduce", "allreduce_resident", "reducescatter", "allgather", "reduce", "broadcast",
+                    choices=["allreduce", "allreduce_resident", "allreduce_mixed", "reducescatter", "allgather", "reduce", "broadcast",
                              "pat_rs", "pat_ag", "sendrecv"])
     ap.add_argument("--root", type=int, default=0)
     ap.add_argument("--shm", required=True)
@@ -46,10 +46,10 @@ def main() -> int:
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
     recv = torch.zeros(n_out, dtype=send.dtype, device=dev)
     torch.cuda.synchronize()
-    resident = a.coll == "allreduce_resident"
+    resident = a.coll in ("allreduce_resident", "allreduce_mixed")
     with ring.PeerRingComm(a.n, a.rank, a.shm, device=ordinal, buff_bytes=a.buff, protocol=a.proto,
                            timeout_ms=20000 if resident else 60000) as comm:
-        if a.coll not in ("allreduce", "allreduce_resident"):
+        if a.coll not in ("allreduce", "allreduce_resident", "allreduce_mixed"):
             for call in range(a.calls):
                 if a.coll == "reducescatter":
                     comm.reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
@@ -71,12 +71,15 @@ def main() -> int:
                                    a.root)
                 np.save(f"{a.out}.{call}.npy", recv.cpu().numpy())
             return 0
-        all_reduce = comm.all_reduce_resident if resident else comm.all_reduce
-        all_reduce(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+        def all_reduce(call):  # allreduce_mixed alternates the host-sequenced and the resident form
+            if a.coll == "allreduce_mixed":
+                return comm.all_reduce_resident if call % 2 else comm.all_reduce
+            return comm.all_reduce_resident if resident else comm.all_reduce
+        all_reduce(0)(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
         np.save(f"{a.out}.0.npy", recv.cpu().numpy())
         for call in range(1, a.calls):
             # in place on the previous result: out_c = allreduce(out_{c-1})
-            all_reduce(recv.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+            all_reduce(call)(recv.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
             np.save(f"{a.out}.{call}.npy", recv.cpu().numpy())
     return 0
 

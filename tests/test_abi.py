@@ -271,6 +271,24 @@ def test_multi_device_validates_before_any_thread(nexr):
         nexr.reduce_copy_multi_device([good], [0, 1], 7, 0)
 
 
+def test_multi_device_sets_validates_every_set_before_any_thread(nexr):
+    """nexrReduceCopyMultiDeviceSets: every work of every set is validated first (a bad work in the
+    last set of the last device fails the call with nothing run); nSets outside [1, 8] is rejected."""
+    L = nexr.lib()
+    good = nexr.make_work([0x1000, 0x2000], [0x3000], 16)
+    bad = nexr.make_work([0x1000, 0], [0x3000], 16)
+    dev = (ctypes.c_int * 2)(0, 0)
+    arr = (nexr.ReduceCopyWork * 6)(good, good, good, good, good, bad)
+    assert L.nexrReduceCopyMultiDeviceSets(arr, dev, 2, 3, 7, 0, 1, None) == 4
+    arr = (nexr.ReduceCopyWork * 1)(good)
+    assert L.nexrReduceCopyMultiDeviceSets(arr, dev, 1, 0, 7, 0, 1, None) == 4   # nSets < 1
+    assert L.nexrReduceCopyMultiDeviceSets(arr, dev, 1, 9, 7, 0, 1, None) == 4   # > NEXR_MAX_MULTI_DEVICE_SETS
+    assert L.nexrReduceCopyMultiDeviceSets(arr, dev, 1, 1, 7, 0, 0, None) == 4   # reps < 1
+    assert L.nexrReduceCopyMultiDeviceSets(None, None, 0, 3, 7, 0, 1, None) == 0
+    with pytest.raises(nexr.NexrError):
+        nexr.reduce_copy_multi_device_sets([[good, good], [good]], [0, 0], 7, 0)
+
+
 @pytest.mark.parametrize("dt", sorted(mg.DT_NAMES) + [10, 11])
 @pytest.mark.parametrize("op,nranks", [(0, 2), (1, 2), (2, 4), (3, 4), (4, 1), (4, 3), (4, 8), (5, 2)])
 def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):

@@ -15,13 +15,22 @@ class _FakeWorkload:
 
     def __init__(self, pkg, cfg, device_index, seed, sets=3):
         self.device_index = device_index
+        self.dev = None
         _FakeWorkload.made.append(device_index)
 
     def work(self, i=0):
-        return ("work", self.device_index)
+        return ("work", self.device_index, i)
 
     def run(self, steps, warmup, dist, per_launch=False):
-        return 0.0, 0.0, 125e-6  # 125 us per launch
+        self.last_set = (steps + warmup - 1) % 3
+        return 2.5e-3, 2.5e-3, 125e-6  # 125 us per launch
+
+    def per_set(self, rounds=6):
+        return {"per_set_us": [125.0, 124.0, 126.0], "per_set_frac": [0.8, 0.81, 0.79], "per_set_launches": rounds,
+                "per_set_buffers_mib": [[0.0, 256.0, 512.0]] * 3}
+
+    def check_exact(self, i):
+        return {"exact": True, "checked_elements": 1 << 20, "checked_set": i}
 
     def free(self):
         pass
@@ -31,7 +40,10 @@ class _FakePkg:
     def __init__(self):
         self.calls = []
 
-    def reduce_copy_multi_device(self, works, devices, dt, op, reps=1):
+    def reduce_copy_multi_device_sets(self, works, devices, dt, op, reps=1):
+        # three rotating sets on every GPU, each GPU's own
+        assert all(len(w) == 3 and [x[2] for x in w] == [0, 1, 2] for w in works)
+        assert [w[0][1] for w in works] == list(devices)
         self.calls.append((list(devices), reps))
         # 0.125 ms per step per GPU alone; 2 % slower with every GPU busy
         per = 0.125e-3 * (1.02 if len(devices) > 1 else 1.0)
@@ -75,7 +87,9 @@ def test_fanout_line_shape(monkeypatch, capsys):
     assert c5["aggregate_over_n_times_n1"] == pytest.approx(1 / 1.02, rel=1e-3)
     assert line["roofline"]["avg_kernel_us"] == 125.0
     assert line["roofline"]["frac"] == pytest.approx(bytes_step / 125e-6 / 1e9 / 8000, abs=1e-4)
-    assert "nexrReduceCopyMultiDevice" in line["config"]["parallelism"]
+    assert "nexrReduceCopyMultiDeviceSets" in line["config"]["parallelism"]
+    assert line["c5"]["sets_per_gpu"] == 3 and "3 rotating" in line["config"]["parallelism"]
+    assert _FakeWorkload.made == [0, 1, 2, 3, 0]  # one 3-set workload per GPU, then GPU 0's roofline leg
 
 
 def test_fanout_refuses_more_gpus_than_visible(monkeypatch):
@@ -192,3 +206,107 @@ def test_side_leg_records_failures():
     r = bench.side_leg(c1_ring)
     assert r["leg"] == "c1_ring" and "peer access refused" in r["error"]
     assert bench.side_leg(lambda a, b: a + b, 2, 3) == 5
+
+
+def test_n1_line_carries_exact_and_per_set(monkeypatch, capsys):
+    """The N=1 line: `exact` (bit-exact check of the last launch's output vs the oracle, outside the
+    timed region) and `roofline.per_set_us` for the headline, and the same keys for every one of
+    the eight extra configurations (a skipped GPUTEST must not leave the bench's work
+    unproven)."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "set_device", lambda *a, **k: None)
+    monkeypatch.setattr(bench, "DeviceWorkload", _FakeWorkload)
+    monkeypatch.setattr(bench, "c1_ring", lambda: {"skipped": "test"})
+    monkeypatch.setattr(bench, "resident_ring", lambda: {"skipped": "test"})
+    res = bench.main_ranks(_args(gpus=1, no_extra=False), bench.CONFIGS["c2"], _FakePkg())
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line == json.loads(json.dumps(res))
+    assert line["exact"] is True and line["exact_check"]["checked_elements"] >= 1 << 20
+    assert line["roofline"]["per_set_us"] == [125.0, 124.0, 126.0] and len(line["roofline"]["per_set_buffers_mib"]) == 3
+    extra = line["extra_configs"]
+    assert sorted(extra) == sorted(bench.EXTRA_ORDER)
+    for name, e in extra.items():
+        assert e["exact"] is True and len(e["per_set_us"]) == 3 and len(e["per_set_frac"]) == 3, name
+
+
+@pytest.mark.parametrize("name", ["c2", "c3_bf16", "c4_i8_min", "c4_i32_prod"])
+def test_check_exact_against_the_oracle_on_cpu_tensors(name):
+    """DeviceWorkload.check_exact itself (CPU tensors standing in for HBM): the output the oracle
+    gives passes, a one-bit flip anywhere in the sample fails, and the sample covers >= 1 Mi elements
+    spread over the buffer including its first and last run."""
+    import numpy as np
+    import torch
+    import oracle
+    cfg = dict(bench.CONFIGS[name])
+    cfg["buf_bytes"] = 8 << 20 if name != "c4_i8_min" else 4 << 20
+    esz = bench.ESZ[cfg["dt"]]
+    n = cfg["buf_bytes"] // esz
+    rng = np.random.default_rng(0)
+    srcs = [torch.from_numpy(rng.integers(0, 256, cfg["buf_bytes"], dtype=np.uint8)) for _ in range(cfg["k"])]
+    if cfg["dt"] in (6, 7, 9):  # finite floats, as the bench's uniform data
+        fl = {6: torch.float16, 7: torch.float32, 9: torch.bfloat16}[cfg["dt"]]
+        srcs = [(torch.rand(n, generator=torch.Generator().manual_seed(i)) * 2 - 1).to(fl) for i in range(cfg["k"])]
+    exp = oracle.reduce_copy([s.view(torch.uint8).numpy() for s in srcs], 1, cfg["dt"], cfg["op"], cfg["arg"])[0]
+    dst = torch.from_numpy(exp.view(np.uint8).copy())
+    wl = object.__new__(bench.DeviceWorkload)
+    wl.cfg, wl.n, wl.dev = cfg, n, torch.device("cpu")
+    wl.sets = [([0] * cfg["k"], [0], srcs, [dst])]
+    r = wl.check_exact(0)
+    assert r["exact"] is True and r["checked_elements"] >= 1 << 20 or r["checked_elements"] == n
+    for pos in (0, n // 2, n - 1):  # first run, a run in the middle (if sampled), last run
+        bad = dst.clone()
+        bad.view(torch.uint8)[pos * esz] ^= 1
+        wl.sets = [([0] * cfg["k"], [0], srcs, [bad])]
+        r2 = wl.check_exact(0, blocks=256, block=64)
+        starts = set(int(x) for x in np.linspace(0, n - 64, 256)) | {0, n - 64}
+        sampled = any(s <= pos < s + 64 for s in starts)
+        assert r2["exact"] is (not sampled), pos
+
+
+def test_xgmi_probe_parts_link_rates_and_timeouts(monkeypatch, capsys):
+    """N>1 with the xGMI probe on (faked: 4 GPUs, faked probe outputs): every part runs in its own
+    bounded subprocess; the remote read/write and every ring result carry their rate against the
+    153 GB/s one-link bound next to their exact check; a part that times out is recorded as such and
+    the headline line is still printed."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(bench, "DeviceWorkload", _FakeWorkload)
+    seen = []
+
+    def fake_bounded(cmd, timeout_s):
+        arg = cmd[2]
+        seen.append((arg, timeout_s))
+        if arg == "--peer-step":
+            return {"gpus": [0, 1], "remote_read": {"xgmi_GBps": 76.5, "exact": True},
+                    "remote_write": {"xgmi_GBps": 122.4, "exact": True}}
+        if arg == "--ring-only":
+            return {"gpus": [0, 1], "exact_all_ranks": True,
+                    "per_protocol_bytes": {"simple": {"4194304": {"ms": 0.1, "algbw_GBps": 41.9, "exact": True}}}}
+        if arg == "--resident-only":
+            return {"ranks": 4, "ch1_4194304": {"ms": 0.2, "algbw_GBps": 20.0, "busbw_GBps": 30.0, "exact": True}}
+        return {"error": f"timeout after {timeout_s:.0f} s"}  # --ring-all hangs
+
+    monkeypatch.setattr(bench, "_bounded", fake_bounded)
+    bench.main_fanout(_args(no_xgmi=False), bench.CONFIGS["c2"], _FakePkg())
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["n_gpus"] == 4 and line["value"] > 0  # the headline is there
+    x = line["xgmi_probe"]
+    assert [a for a, _ in seen] == ["--peer-step", "--ring-only", "--resident-only", "--ring-all"]
+    assert all(t <= 100 for _, t in seen)
+    assert x["link_bound_GBps"] == 153.0
+    assert x["remote_read"]["frac_of_link"] == pytest.approx(76.5 / 153, abs=1e-4)
+    assert x["remote_write"]["frac_of_link"] == pytest.approx(122.4 / 153, abs=1e-4)
+    r = x["ring_processes"]["per_protocol_bytes"]["simple"]["4194304"]
+    assert r["busbw_GBps"] == pytest.approx(41.9, abs=0.01) and r["frac_of_link"] == pytest.approx(41.9 / 153, abs=1e-3)
+    assert x["resident_ring"]["ch1_4194304"]["frac_of_link"] == pytest.approx(30 / 153, abs=1e-3)
+    assert "timeout" in x["ring_processes_all_gpus"]["error"]
+
+
+def test_xgmi_probe_skipped_on_one_gpu(monkeypatch):
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    calls = []
+    monkeypatch.setattr(bench, "_bounded", lambda cmd, t: calls.append(cmd) or {"skipped": "needs 2 GPUs, found 1"})
+    res = bench.xgmi_probe()
+    assert "skipped" in res and len(calls) == 1

@@ -86,3 +86,25 @@ def test_healthy_comm_after_a_broken_one(ring, oracle):
         o = [np.zeros(count, np.uint32) for _ in range(n)]
         comm.all_reduce([v.ctypes.data for v in x], [v.ctypes.data for v in o], count, U32, 0)
         assert all(np.array_equal(v, np.arange(count, dtype=np.uint32) * 6) for v in o)
+
+
+@pytest.mark.parametrize("kind", ["ring", "tree", "pat_rs", "pat_ag", "sendrecv"])
+@pytest.mark.parametrize("at", [1, 3])
+def test_thread_spawn_failure_returns_system_error(ring, oracle, nexr, kind, at, monkeypatch):
+    """runThreads (nexr_ring.cpp) when the k-th rank thread cannot be created (test hook
+    NEXR_TEST_SPAWN_FAIL_AT, std::system_error as from std::thread): the threads already started see
+    the abort and leave at once, the call returns ncclSystemError (2) instead of letting the exception
+    cross the C entry point (std::terminate), and the communicator is marked broken."""
+    n, count = 4, 20_000
+    good = Injector(oracle, at=-1, mode="fail")
+    with ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, good.address, 20000, 0, None, None, 2) as comm:
+        monkeypatch.setenv("NEXR_TEST_SPAWN_FAIL_AT", str(at))
+        t0 = time.perf_counter()
+        with pytest.raises(nexr.NexrError) as e:
+            _run(comm, kind, n, count)
+        assert e.value.code == nexr.Result.SystemError
+        assert time.perf_counter() - t0 < 5  # far below the 20 s wait bound: the started ranks aborted
+        monkeypatch.delenv("NEXR_TEST_SPAWN_FAIL_AT")
+        with pytest.raises(nexr.NexrError) as e2:
+            _run(comm, kind, n, count)
+        assert e2.value.code == nexr.Result.InvalidUsage

@@ -97,6 +97,23 @@ def test_peer_ring_resident_processes(oracle, tmp_path, n, dt, op):
         assert mg.canon_bytes(dt, outs[r][1]) == mg.canon_bytes(dt, exp1[r]), f"rank {r}, call 1 (in place)"
 
 
+@pytest.mark.parametrize("n,dt,op", [(2, mg.F32, 0), (3, mg.I32, 0)])
+def test_peer_ring_alternating_host_and_resident(oracle, tmp_path, n, dt, op):
+    """The ring link r -> r+1 serves the host-sequenced and the resident all-reduce, each with its own
+    step counters. Four calls on one communicator, host / resident / host / resident, each in place on
+    the previous result: every switch waits until the next rank has consumed what the other form sent
+    (ringLinkHandover, nexr_ring.cpp), so no slot is overwritten before it is read. Each call equals
+    the fold-order oracle of its input."""
+    from oracle.ring import ring_allreduce_expected
+    count, buff, calls = 200_003, 1 << 18, 4
+    outs = _run_ring(tmp_path, n, dt, op, count, 0, buff, calls=calls, coll="allreduce_mixed")
+    cur = mg.gen_inputs(dt, n, count, 7, special=True)
+    for c in range(calls):
+        cur = ring_allreduce_expected([cur[r] for r in range(n)], dt, op, buff)
+        for r in range(n):
+            assert mg.canon_bytes(dt, outs[r][c]) == mg.canon_bytes(dt, cur[r]), f"rank {r}, call {c}"
+
+
 def test_peer_ring_c1_two_processes_fp32_sum(tmp_path):
     # BASELINE configs[0] (fp32 sum all-reduce, 4 MiB, 2 ranks) with real process ranks.
     count = 1 << 20

@@ -12,7 +12,8 @@ fp32 sum, 256 MiB per buffer. Then the process-rank ring itself across the two G
 (nexrPeerRingCommCreate), run the emulated ring all-reduce (C1's 4 MiB and 64 MiB of fp32 per rank,
 SIMPLE; LL and LL128 at 4 MiB) with every step's reduce-copy writing into the peer GPU's HBM over
 xGMI; every rank's result is checked exactly (integer-valued inputs). `--ring-all N` runs the same
-ring with N processes on the first N GPUs. Prints one JSON line; with fewer than two GPUs it prints a
+ring with N processes on the first N GPUs; `--peer-step` runs only the three kernel legs (bench.py
+runs each part as its own bounded subprocess). Prints one JSON line; with fewer than two GPUs it prints a
 "skipped" line and exits 0. bench.py runs it as bounded subprocesses when it drives more than one
 GPU, so a failure here can never take the bench line down with it.
 """
@@ -26,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main() -> int:
+def main(peer_step_only: bool = False) -> int:
     import torch
 
     n_dev = torch.cuda.device_count()
@@ -85,11 +86,12 @@ def main() -> int:
     ok_write = torch.equal(o1.to(d0), a0 + b0)
     out["remote_write"] = {"us": round(t * 1e6, 1), "xgmi_GBps": round(buf / t / 1e9, 1),
                            "alg_GBps": round(3 * buf / t / 1e9, 1), "exact": bool(ok_write)}
-    out["ring_processes"] = ring_processes()
-    try:
-        out["resident_ring"] = resident_ring(min(n_dev, 8))
-    except Exception as e:  # noqa: BLE001 - reported, never raised
-        out["resident_ring"] = {"error": repr(e)[:300]}
+    if not peer_step_only:
+        out["ring_processes"] = ring_processes()
+        try:
+            out["resident_ring"] = resident_ring(min(n_dev, 8))
+        except Exception as e:  # noqa: BLE001 - reported, never raised
+            out["resident_ring"] = {"error": repr(e)[:300]}
     print(json.dumps(out), flush=True)
     return 0
 
@@ -217,4 +219,4 @@ if __name__ == "__main__":
     if "--ring-rank" in a:
         sys.exit(ring_rank(int(a[a.index("--ring-rank") + 1]), int(a[a.index("--ranks") + 1]),
                            a[a.index("--shm") + 1], [int(v) for v in a[a.index("--counts") + 1].split(",")]))
-    sys.exit(main())
+    sys.exit(main(peer_step_only="--peer-step" in a))
