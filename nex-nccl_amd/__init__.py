@@ -138,6 +138,32 @@ def hip_runtime() -> ctypes.CDLL:
     return ctypes.CDLL(paths[0])
 
 
+def _preload_hip_runtime() -> None:
+    """One HIP runtime per process. torch ships its own libamdhip64 (soname libamdhip64.so.7, NEEDED
+    by torch as "libamdhip64.so" through its RUNPATH), so loading libnexr first would map
+    /opt/rocm's runtime and torch then a second one: torch's streams and allocations would be
+    foreign handles to libnexr (hipErrorNoDevice / invalid handle at the first launch). When a
+    runtime is already mapped (torch imported, or any other), libnexr's NEEDED libamdhip64.so.7
+    resolves to it. Otherwise, if torch is installed, its runtime file is mapped here by path,
+    without importing torch: libnexr then binds to it through the soname, and a later `import
+    torch` finds that same file already mapped. Without torch, /opt/rocm's runtime serves."""
+    with open("/proc/self/maps") as f:
+        if any("libamdhip64" in ln for ln in f):
+            return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        cand = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def lib() -> ctypes.CDLL:
     """Load libnexr.so (raises if it is missing: there is no CPU fallback)."""
     global _lib
@@ -146,15 +172,7 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise NexrError(Result.InternalError,
                         f"{LIB_PATH} not built (run __graft_entry__.build() or make -C nex-nccl_amd/csrc)")
-    # One HIP runtime per process. torch ships its own libamdhip64 (soname libamdhip64.so.7, but
-    # NEEDED by torch as "libamdhip64.so"), so loading libnexr first maps /opt/rocm's runtime and
-    # torch then maps a second one: torch's streams and allocations are then foreign handles to
-    # libnexr (hipErrorNoDevice / invalid handle at the first launch). Loading torch first makes
-    # libnexr's NEEDED libamdhip64.so.7 resolve to the runtime torch already mapped.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    _preload_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
     vp, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
     P = ctypes.POINTER
