@@ -1,0 +1,38 @@
+"""profiles/ stays an index of evidence, not an archive: every file under
+profiles/ is listed in profiles/INDEX.md under the claim it backs, INDEX.md is current, and every
+profiles file DESIGN.md cites exists (brace and <config> patterns expanded)."""
+import fnmatch
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import profiles_index  # noqa: E402
+
+
+def test_index_lists_every_file_and_is_current():
+    assert profiles_index.check() == []
+
+
+def _expand(t):
+    m = re.search(r"\{([^{}]*)\}", t)
+    if not m:
+        return [t]
+    return [x for alt in m.group(1).split(",") for x in _expand(t[:m.start()] + alt + t[m.end():])]
+
+
+def test_design_citations_resolve():
+    text = open(os.path.join(ROOT, "DESIGN.md")).read()
+    files = os.listdir(os.path.join(ROOT, "profiles"))
+    toks = set(re.findall(r"`(?:profiles/)?((?:r0\d|pmc_)[^`\s]*)`", text))
+    toks |= {t for t in re.findall(r"profiles/([^\s`]+)", text)}
+    missing = []
+    for t in toks:
+        t = t.rstrip(".,;:)")
+        if "{" in t and "}" not in t:
+            continue  # a brace list cut by the prose regex; the backticked form is checked
+        pats = [re.sub(r"<[^>]*>", "*", e) for e in _expand(t)]
+        if not any(fnmatch.fnmatch(f, p) or fnmatch.fnmatch(f, p + "*") for p in pats for f in files):
+            missing.append(t)
+    assert not missing, missing
