@@ -93,6 +93,61 @@ def report(name, cases, times, bytes_per_launch, kind):
         print(json.dumps(rec), flush=True)
 
 
+def hybrids(name, tsets, times, k, n, dtid, bpl, rounds):
+    """Which buffers make a set fast or slow: the fastest and slowest torch sets, and sets built from
+    the fast set's sources with the slow set's destination (and the reverse), half of each set's
+    sources swapped, and each single source of the fast set swapped for the slow set's."""
+    med = {c["label"]: statistics.median(times[c["label"]]) for c in tsets}
+    fast = min(tsets, key=lambda c: med[c["label"]])
+    slow = max(tsets, key=lambda c: med[c["label"]])
+    h = k // 2
+    mk = lambda lab, sp, dp: {"label": lab, "sp": sp, "dp": dp, "n": n}  # noqa: E731
+    cases = [mk("fast", fast["sp"], fast["dp"]), mk("slow", slow["sp"], slow["dp"]),
+             mk("fast_srcs_slow_dst", fast["sp"], slow["dp"]), mk("slow_srcs_fast_dst", slow["sp"], fast["dp"]),
+             mk("fast_first_half_srcs", fast["sp"][:h] + slow["sp"][h:], fast["dp"]),
+             mk("fast_second_half_srcs", slow["sp"][:h] + fast["sp"][h:], fast["dp"])]
+    for j in range(k):
+        sp = list(fast["sp"])
+        sp[j] = slow["sp"][j]
+        cases.append(mk(f"fast_with_slow_src{j}", sp, fast["dp"]))
+    t = run_cases(name, cases, rounds, dtid)
+    print(json.dumps({"probe": name, "kind": "hybrid_sets", "fast": fast["label"], "slow": slow["label"]}), flush=True)
+    report(name, cases, t, bpl, "hybrid")
+
+
+def per_buffer(name, tsets, n, dt, dtid, esz, rounds):
+    """Every buffer of the torch sets alone: a K = 1 copy from it into one fixed scratch buffer, and
+    a copy from a fixed source into it — a buffer whose own placement is slow shows here."""
+    stream = torch.cuda.current_stream()
+    h = stream.cuda_stream
+    scratch = torch.empty(n, dtype=dt, device="cuda")
+    fixed = torch.empty(n, dtype=dt, device="cuda")
+    fixed.zero_()
+    bufs = []
+    for c in tsets:
+        for j, p in enumerate(c["sp"] + c["dp"]):
+            bufs.append((f"{c['label']}.{j}", p))
+    res = {lab: {"read": [], "write": []} for lab, _ in bufs}
+    for _ in range(max(3, rounds // 3)):
+        evs = []
+        for lab, p in bufs:
+            for kind, sp, dp in (("read", [p], [scratch.data_ptr()]), ("write", [fixed.data_ptr()], [p])):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                nexr.reduce_copy_ptrs(sp, dp, n, dtid, 0, 0, None, False, h)
+                e1.record(stream)
+                evs.append((lab, kind, e0, e1))
+        torch.cuda.synchronize()
+        for lab, kind, e0, e1 in evs:
+            res[lab][kind].append(e0.elapsed_time(e1) * 1e3)
+    for lab, _ in bufs:
+        r = res[lab]
+        print(json.dumps({"probe": name, "kind": "per_buffer_copy", "buffer": lab,
+                          "copy_from_us": round(statistics.median(r["read"]), 2),
+                          "copy_into_us": round(statistics.median(r["write"]), 2)}), flush=True)
+    del scratch, fixed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c3_bf16,c2")
@@ -136,6 +191,8 @@ def main():
         torch.cuda.synchronize()
         times = run_cases(name, cases, args.rounds, dtid)
         report(name, cases, times, bpl, "rate")
+        hybrids(name, cases[:args.torch_sets], times, k, n, dtid, bpl, args.rounds)
+        per_buffer(name, cases[:args.torch_sets], n, dt, dtid, esz, args.rounds)
         first = cases[0]["dst"]
         same = all(torch.equal(c["dst"], first) for c in cases[1:])
         print(json.dumps({"probe": name, "all_outputs_identical": bool(same)}), flush=True)
