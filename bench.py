@@ -756,10 +756,11 @@ def main_ranks(args, cfg, pkg) -> dict | None:
     bytes_step = algorithmic_bytes(cfg)
     value = dist.world * bytes_step * args.steps / max_s / 1e9
     ranks = dist.gather([local_s, kernel_s], wl.dev)
-    sets = exact = None
-    if dist.rank == 0:  # after the timed region: per-set times and the bit-exact check of the last output
-        sets = side_leg(wl.per_set)
-        exact = side_leg(wl.check_exact, wl.last_set)
+    # After the timed region: every rank checks its own last output bit-exactly against the oracle;
+    # rank 0 also times each of its rotating sets.
+    exact = side_leg(wl.check_exact, wl.last_set)
+    exact_ranks = [f[0] == 1.0 for f in dist.gather([1.0 if exact.get("exact") is True else 0.0], wl.dev)]
+    sets = side_leg(wl.per_set) if dist.rank == 0 else None
     c5 = None
     if dist.world > 1:
         # Same-run legs: rank 0's GPU alone (the N=1 reference), then every GPU alone in turn.
@@ -783,8 +784,8 @@ def main_ranks(args, cfg, pkg) -> dict | None:
                             if torch.cuda.device_count() < dist.world else ""))
         result["roofline"] = roofline(cfg, args.config, kernel_s, per_launch)
         result["roofline"].update(sets if "error" not in sets else {"per_set_error": sets})
-        result["exact"] = exact.get("exact")
-        result["exact_check"] = exact
+        result["exact"] = all(exact_ranks)
+        result["exact_check"] = dict(exact, per_rank=exact_ranks)
         result["cpu_baseline"] = None
         result["h2d_inclusive"] = None
         if dist.world == 1:
@@ -841,13 +842,21 @@ def main_fanout(args, cfg, pkg) -> dict:
                        f"independent chunks x{args.gpus} (no collective), one process, "
                        f"nexrReduceCopyMultiDeviceSets (a host thread + stream per GPU, {FANOUT_SETS} rotating sets)" +
                        (f"; REHEARSAL: {args.gpus} chunks folded onto {n_vis} GPU(s)" if n_vis < args.gpus else ""))
+    # Every GPU's output against the oracle (outside the timed legs; each set holds its last output).
+    checks = [side_leg(wl.check_exact, 0) for wl in wls]
+    result["exact"] = all(c.get("exact") is True for c in checks)
+    result["exact_check"] = {"per_gpu": [c.get("exact") for c in checks],
+                             "checked_elements_per_gpu": checks[0].get("checked_elements"),
+                             "check": checks[0].get("check", checks[0].get("error"))}
     # Roofline of the kernel itself: HIP events on GPU 0's launch stream, 3 rotating sets.
     for wl in wls:
         wl.free()
     wl0 = DeviceWorkload(pkg, cfg, 0, seed=1000)
     _, _, kernel_s = wl0.run(args.steps, args.warmup, _Solo())
+    sets = side_leg(wl0.per_set)
     wl0.free()
     result["roofline"] = roofline(cfg, args.config, kernel_s)
+    result["roofline"].update(sets if "error" not in sets else {"per_set_error": sets})
     result["cpu_baseline"] = None
     result["h2d_inclusive"] = None
     result["c5"] = c5_summary(args.gpus, bytes_step, args.steps, agg_s, solo[0], solo)

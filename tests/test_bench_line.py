@@ -90,6 +90,8 @@ def test_fanout_line_shape(monkeypatch, capsys):
     assert "nexrReduceCopyMultiDeviceSets" in line["config"]["parallelism"]
     assert line["c5"]["sets_per_gpu"] == 3 and "3 rotating" in line["config"]["parallelism"]
     assert _FakeWorkload.made == [0, 1, 2, 3, 0]  # one 3-set workload per GPU, then GPU 0's roofline leg
+    assert line["exact"] is True and line["exact_check"]["per_gpu"] == [True] * 4
+    assert line["roofline"]["per_set_us"] == [125.0, 124.0, 126.0]
 
 
 def test_fanout_refuses_more_gpus_than_visible(monkeypatch):
