@@ -697,6 +697,11 @@ nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
 // rank writes the link as the other user, it waits until rank r+1 has consumed everything the
 // previous user sent: head == tail after host-sequenced calls, or rank r+1's kernel done after
 // resident ones. Bounded by the communicator's timeout and its abort word, as every other wait.
+bool envFlagOn(const char* name, bool dflt) {
+  const char* v = getenv(name);
+  return v && *v ? v[0] != '0' : dflt;
+}
+
 nexrResult_t ringLinkHandover(nexrRingComm* c, bool resident) {
   const int want = resident ? 2 : 1;
   const int prev = c->ringLinkUser;
@@ -1192,8 +1197,12 @@ nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* 
   // Wait for the kernel while relaying the communicator's abort word (set by a failing rank in another
   // process) into this GPU's status word, which the kernel's waits poll: a rank's failure then ends
   // every rank's kernel at once instead of after the full timeout.
+  // Poll without sleeping for the first 2 ms (a C1-size call takes tens of microseconds, and a sleep
+  // costs the timer slack, ~50 us), then every 20 us.
   PeerHeader* ph = peerHeader(c->shm);
-  for (bool relayed = false; r == nexrSuccess;) {
+  const auto pollStart = std::chrono::steady_clock::now();
+  static const bool relay = envFlagOn("NEXR_RESIDENT_RELAY", true);  // A/B knob (tools/xgmi_probe.py)
+  for (bool relayed = !relay; r == nexrSuccess && relay;) {
     const hipError_t q = hipStreamQuery(s);
     if (q == hipSuccess) break;
     if (q != hipErrorNotReady) {
@@ -1204,7 +1213,10 @@ nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* 
       __atomic_store_n(c->resStatus[0], 2u, __ATOMIC_RELEASE);
       relayed = true;
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(5));
+    if (std::chrono::steady_clock::now() - pollStart > std::chrono::milliseconds(2))
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else
+      std::this_thread::yield();
   }
   if (hipStreamSynchronize(s) != hipSuccess && r == nexrSuccess) r = nexrUnhandledCudaError;
   if (r == nexrSuccess && __atomic_load_n(c->resStatus[0], __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
