@@ -171,6 +171,40 @@ def test_multi_device_independent_chunks_match_oracle(nexr, oracle, dt, dev):
             w.check((mg.DT_NAMES[dt], name, i, w.n))
 
 
+@pytest.mark.parametrize("dt", [mg.F32, mg.BF16, mg.I8])
+def test_multi_device_sets_rotate_and_match_oracle(nexr, oracle, dt, dev):
+    """nexrReduceCopyMultiDeviceSets (the C5 fan-out's rotation): three sets of works per thread,
+    launch k running set k mod 3; with reps = 4 every set runs at least once, and every set's output
+    matches the oracle (mixed K, M, sizes and pointer phases across the sets); reps = 2 leaves the
+    third set untouched (its guard-filled outputs unchanged), which shows the rotation order."""
+    rng = np.random.default_rng(900 + dt)
+    n_dev = torch.cuda.device_count()
+    threads = 2
+    per_dev = []
+    for t in range(threads):
+        with torch.cuda.device(t % n_dev):
+            per_dev.append([_Work(nexr, oracle, dt, mg.SUM, "sum", int(rng.integers(1, 9)), int(rng.integers(1, 3)),
+                                  int(rng.choice([17, 4097, 300_001])), 8000 + 10 * t + s, rng,
+                                  ["zero", "phase", "random"][s]) for s in range(3)])
+    torch.cuda.synchronize()
+    devices = [t % n_dev for t in range(threads)]
+    nexr.reduce_copy_multi_device_sets([[w.work for w in ws] for ws in per_dev], devices, dt, mg.SUM, reps=4)
+    for t, ws in enumerate(per_dev):
+        for s, w in enumerate(ws):
+            w.check((mg.DT_NAMES[dt], "thread", t, "set", s))
+    # reps = 2 on fresh outputs: sets 0 and 1 run, set 2 is never launched
+    for ws in per_dev:
+        for w in ws:
+            for b in w.dbufs:
+                b.fill_(0x5A)
+    torch.cuda.synchronize()
+    nexr.reduce_copy_multi_device_sets([[w.work for w in ws] for ws in per_dev], devices, dt, mg.SUM, reps=2)
+    for t, ws in enumerate(per_dev):
+        ws[0].check((mg.DT_NAMES[dt], "reps 2, thread", t, "set 0"))
+        ws[1].check((mg.DT_NAMES[dt], "reps 2, thread", t, "set 1"))
+        assert all((b.cpu().numpy() == 0x5A).all() for b in ws[2].dbufs), "set 2 ran with reps = 2"
+
+
 def test_multi_device_rejects_bad_ordinals(nexr, dev):
     x = torch.ones(1024, device="cuda")
     y = torch.empty_like(x)
