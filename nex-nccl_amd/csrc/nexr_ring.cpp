@@ -690,6 +690,11 @@ nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
   return nexrSuccess;
 }
 
+bool envFlagOn(const char* name, bool dflt) {
+  const char* v = getenv(name);
+  return v && *v ? v[0] != '0' : dflt;
+}
+
 // Process ranks: the ring link r -> r+1 (rank r+1's receive FIFO) serves two users with separate
 // step counters: the host-sequenced collectives (head/tail in the shared segment, also PAT's ring
 // link) and the resident all-reduce (records behind the FIFO). Either returns once this rank's own
@@ -697,11 +702,6 @@ nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p) {
 // rank writes the link as the other user, it waits until rank r+1 has consumed everything the
 // previous user sent: head == tail after host-sequenced calls, or rank r+1's kernel done after
 // resident ones. Bounded by the communicator's timeout and its abort word, as every other wait.
-bool envFlagOn(const char* name, bool dflt) {
-  const char* v = getenv(name);
-  return v && *v ? v[0] != '0' : dflt;
-}
-
 nexrResult_t ringLinkHandover(nexrRingComm* c, bool resident) {
   const int want = resident ? 2 : 1;
   const int prev = c->ringLinkUser;
