@@ -10,7 +10,7 @@ Infinity-Cache-resident bytes. With N GPUs every GPU runs its own independent 25
 
     python bench.py                                    # N=1 (+ C3/C4 extra configs, CPU baseline)
     torchrun --nproc-per-node N bench.py --gpus N      # one process per GPU; gloo (CPU) barrier/max
-    python bench.py --gpus N                           # one process: nexrReduceCopyMultiDevice,
+    python bench.py --gpus N                           # one process: nexrReduceCopyMultiDeviceSets,
                                                        #   a host thread + stream per GPU
 Either N > 1 way also times an N=1 leg on GPU 0 in the same run, and every GPU alone, and reports
 them beside the aggregate under `c5`.
@@ -211,12 +211,17 @@ class DeviceWorkload:
         return self.pkg.make_work(sp, dp, self.n, self.cfg["arg"])
 
     def per_set(self, rounds: int = 6) -> dict:
-        """After the timed region: `rounds` x sets more launches, round-robin over the sets as in the
-        timed loop, with HIP events around every launch on the launch stream; the average kernel
-        time of each set and where its buffers sit (the same kernel ran one set of C3 at
-        0.81-0.83 of peak and the other two at 0.75-0.77)."""
+        """After the timed region (and after check_exact: it overwrites the outputs): `rounds` x sets
+        more launches, round-robin over the sets as in the timed loop, with HIP events around every
+        launch on the launch stream; the average kernel time of each set and where its buffers sit
+        (the same kernel ran one set of C3 at 0.81-0.83 of peak and the other two at
+        0.75-0.77). Each launch is followed by the same bytes as a uint32 sum (the cheapest fold,
+        v_add_u32, at that datatype's own geometry) on the same buffers: the rate this placement gives
+        the same K + M streams, so `kernel_over_u32_sum` says what the configuration's arithmetic
+        costs over the bare streams."""
         import torch
         cfg, ns = self.cfg, len(self.sets)
+        n32 = cfg["buf_bytes"] // 4
         evs = []
         with torch.cuda.device(self.dev):
             # one untimed launch first: the first launch after the GPU idled runs a few % slow, and
@@ -225,20 +230,25 @@ class DeviceWorkload:
             self.pkg.reduce_copy_ptrs(sp, dp, self.n, cfg["dt"], cfg["op"], cfg["arg"], None, False, self.handle)
             for i in range(rounds * ns):
                 sp, dp, _, _ = self.sets[i % ns]
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(self.stream)
-                self.pkg.reduce_copy_ptrs(sp, dp, self.n, cfg["dt"], cfg["op"], cfg["arg"], None, False, self.handle)
-                e1.record(self.stream)
-                evs.append((i % ns, e0, e1))
+                for kind, n, dt, op, arg in (("kernel", self.n, cfg["dt"], cfg["op"], cfg["arg"]), ("u32", n32, 3, 0, 0)):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(self.stream)
+                    self.pkg.reduce_copy_ptrs(sp, dp, n, dt, op, arg, None, False, self.handle)
+                    e1.record(self.stream)
+                    evs.append((kind, i % ns, e0, e1))
             torch.cuda.synchronize(self.dev)
-        us = [[] for _ in range(ns)]
-        for k, e0, e1 in evs:
-            us[k].append(e0.elapsed_time(e1) * 1e3)
+        us = {"kernel": [[] for _ in range(ns)], "u32": [[] for _ in range(ns)]}
+        for kind, k, e0, e1 in evs:
+            us[kind][k].append(e0.elapsed_time(e1) * 1e3)
+        mean = lambda v: sum(v) / len(v)  # noqa: E731
+        ker, u32 = [mean(u) for u in us["kernel"]], [mean(u) for u in us["u32"]]
         lo = min(p for sp, dp, _, _ in self.sets for p in sp + dp)
-        return {"per_set_us": [round(sum(u) / len(u), 2) for u in us],
-                "per_set_frac": [round(algorithmic_bytes(cfg) / (sum(u) / len(u)) / 1e3 / PEAK_HBM_GBS, 4) for u in us],
+        return {"per_set_us": [round(x, 2) for x in ker],
+                "per_set_frac": [round(algorithmic_bytes(cfg) / x / 1e3 / PEAK_HBM_GBS, 4) for x in ker],
                 "per_set_launches": rounds,
-                "per_set_buffers_mib": [[round((p - lo) / (1 << 20), 3) for p in sp + dp] for sp, dp, _, _ in self.sets]}
+                "per_set_buffers_mib": [[round((p - lo) / (1 << 20), 3) for p in sp + dp] for sp, dp, _, _ in self.sets],
+                "same_bytes_u32_sum_per_set_us": [round(x, 2) for x in u32],
+                "kernel_over_u32_sum": round(mean(ker) / mean(u32), 4)}
 
     def check_exact(self, i: int, blocks: int = 256, block: int = 4096) -> dict:
         """Test infrastructure, outside every timed region: the output of set `i` (every set holds the
@@ -334,8 +344,8 @@ def extra_configs(pkg, steps: int = 20, warmup: int = 5, names=EXTRA_ORDER) -> d
         cfg = CONFIGS[name]
         wl = DeviceWorkload(pkg, cfg, local_device_index(), seed=2000 + i)
         _, _, kernel_s = wl.run(steps, warmup, _Solo())
-        sets = side_leg(wl.per_set)
         exact = side_leg(wl.check_exact, wl.last_set)
+        sets = side_leg(wl.per_set)
         wl.free()
         r = roofline(cfg, name, kernel_s)
         out[name] = {"workload": cfg["workload"], "dtype": cfg["dtype"], "bytes_per_launch": algorithmic_bytes(cfg),
