@@ -224,10 +224,11 @@ class DeviceWorkload:
         n32 = cfg["buf_bytes"] // 4
         evs = []
         with torch.cuda.device(self.dev):
-            # one untimed launch first: the first launch after the GPU idled runs a few % slow, and
-            # would otherwise always land on set 0
+            # untimed launches first: the first launch after the GPU idled runs a few % slow and would
+            # otherwise always land on set 0, and the uint32 kernel's first launch loads its code object
             sp, dp, _, _ = self.sets[-1]
             self.pkg.reduce_copy_ptrs(sp, dp, self.n, cfg["dt"], cfg["op"], cfg["arg"], None, False, self.handle)
+            self.pkg.reduce_copy_ptrs(sp, dp, n32, 3, 0, 0, None, False, self.handle)
             for i in range(rounds * ns):
                 sp, dp, _, _ = self.sets[i % ns]
                 for kind, n, dt, op, arg in (("kernel", self.n, cfg["dt"], cfg["op"], cfg["arg"]), ("u32", n32, 3, 0, 0)):
