@@ -690,6 +690,7 @@ def h2d_inclusive(pkg, cfg, reps: int = 3):
     for s in pinned_s:
         s.random_(0, 255)
     t_pin = run(pinned_s, pinned_d)
+    split = side_leg(explicit_copies, pkg, cfg, pinned_s, pinned_d, reps)
     del pinned_s, pinned_d
     rng = np.random.default_rng(3)
     page_s = [rng.integers(0, 256, cfg["buf_bytes"], dtype=np.uint8) for _ in range(cfg["k"])]
@@ -698,11 +699,52 @@ def h2d_inclusive(pkg, cfg, reps: int = 3):
     alg = algorithmic_bytes(cfg)
     return {"value": round(alg / t_pin / 1e9, 2), "unit": "GB/s", "ms_per_call": round(t_pin * 1e3, 3),
             "path": "nexrReduceCopyHost, pinned host buffers: zero-copy kernel over PCIe Gen5 x16",
+            "explicit_copies": split,
             "pageable": {"value": round(alg / t_page / 1e9, 2), "ms_per_call": round(t_page * 1e3, 3),
                          "path": "host copy team (8 threads) into pinned zero-copy slots, 32 MiB chunks, "
                                  "kernel over PCIe, copy team out (the path for calls of 256 MiB or more; "
                                  "4-256 MiB: runtime H2D -> kernel -> D2H chunk pipeline; up to 4 MiB: the "
                                  "calling thread's copies into zero-copy slots)"}}
+
+
+def explicit_copies(pkg, cfg, pinned_s, pinned_d, reps: int = 3) -> dict:
+    """SURVEY §8(d)'s H<->D-inclusive measurement as stated: K H2D copies from pinned host buffers
+    (hipMemcpyAsync), the kernel on the device copies, M D2H copies, one stream, timed end to end with
+    HIP events between the phases, so the copy / kernel split is reported. The zero-copy path above
+    (`value`) overlaps the two PCIe directions and is the faster way to run the same call."""
+    import torch
+    n = cfg["buf_bytes"] // ESZ[cfg["dt"]]
+    dev = torch.device("cuda", local_device_index())
+    stream = torch.cuda.current_stream(dev)
+    d_s = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8, device=dev) for _ in pinned_s]
+    d_d = [torch.empty(cfg["buf_bytes"], dtype=torch.uint8, device=dev) for _ in pinned_d]
+    sp, dp = [t.data_ptr() for t in d_s], [t.data_ptr() for t in d_d]
+    phases = {"h2d": [], "kernel": [], "d2h": []}
+    with torch.cuda.device(dev):
+        for it in range(reps + 1):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(stream)
+            for d, h in zip(d_s, pinned_s):
+                d.copy_(h, non_blocking=True)
+            ev[1].record(stream)
+            pkg.reduce_copy_ptrs(sp, dp, n, cfg["dt"], cfg["op"], cfg["arg"], None, False, stream.cuda_stream)
+            ev[2].record(stream)
+            for h, d in zip(pinned_d, d_d):
+                h.copy_(d, non_blocking=True)
+            ev[3].record(stream)
+            ev[3].synchronize()
+            if it:  # the first round warms the copy path
+                for k, (a, b) in zip(("h2d", "kernel", "d2h"), zip(ev[:3], ev[1:])):
+                    phases[k].append(a.elapsed_time(b))
+    ms = {k: sum(v) / len(v) for k, v in phases.items()}
+    total = sum(ms.values())
+    return {"value": round(algorithmic_bytes(cfg) / (total / 1e3) / 1e9, 2), "unit": "GB/s",
+            "ms_per_call": round(total, 3), "h2d_ms": round(ms["h2d"], 3), "kernel_ms": round(ms["kernel"], 4),
+            "d2h_ms": round(ms["d2h"], 3),
+            "h2d_gbs": round(cfg["k"] * cfg["buf_bytes"] / (ms["h2d"] / 1e3) / 1e9, 2),
+            "d2h_gbs": round(cfg["m"] * cfg["buf_bytes"] / (ms["d2h"] / 1e3) / 1e9, 2),
+            "path": f"{cfg['k']} hipMemcpyAsync H2D from pinned buffers -> nexrReduceCopy on device copies -> "
+                    f"{cfg['m']} D2H, one stream, HIP events between the phases"}
 
 
 def h2d_pinned_all_ranks(pkg, cfg, dist, device, reps: int = 3) -> dict:
