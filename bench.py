@@ -642,9 +642,10 @@ def xgmi_link_rates(res: dict) -> dict:
 def xgmi_probe(budget_s: float = 240.0):
     """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, each part in a
     bounded subprocess of its own so one hang cannot cost the others or the line: GPU 0's kernel with
-    an operand in GPU 1's HBM, the two-rank process ring, the resident ring over all GPUs, and with
-    three or more GPUs the process ring over all of them (up to 8). The parts share `budget_s`; a part
-    that times out is recorded as such. Reported, never allowed to fail the bench line."""
+    an operand in GPU 1's HBM, the two-rank process ring, the resident ring over all GPUs (only with
+    NEXR_XGMI_RESIDENT=1: frozen, beyond §8), and with three or more GPUs the process ring over all
+    of them (up to 8). The parts share `budget_s`; a part that times out is recorded as such.
+    Reported, never allowed to fail the bench line."""
     import torch
     probe = os.path.join(ROOT, "tools", "xgmi_probe.py")
     t_end = time.perf_counter() + budget_s
@@ -659,7 +660,10 @@ def xgmi_probe(budget_s: float = 240.0):
     res = part(["--peer-step"], 60.0)
     if isinstance(res, dict) and "skipped" not in res:
         res["ring_processes"] = part(["--ring-only"], 75.0)
-        res["resident_ring"] = part(["--resident-only", str(min(n_dev, 8))], 60.0)
+        # The device-resident collectives go beyond SURVEY §8 and are frozen: their
+        # cross-GPU run is opt-in, so the default line spends its probe budget on row f4 only.
+        if os.environ.get("NEXR_XGMI_RESIDENT") == "1":
+            res["resident_ring"] = part(["--resident-only", str(min(n_dev, 8))], 60.0)
         if n_dev >= 3:
             res["ring_processes_all_gpus"] = part(["--ring-all", str(min(n_dev, 8))], 100.0)
     return xgmi_link_rates(res)

@@ -290,6 +290,7 @@ def test_xgmi_probe_parts_link_rates_and_timeouts(monkeypatch, capsys):
         return {"error": f"timeout after {timeout_s:.0f} s"}  # --ring-all hangs
 
     monkeypatch.setattr(bench, "_bounded", fake_bounded)
+    monkeypatch.setenv("NEXR_XGMI_RESIDENT", "1")
     bench.main_fanout(_args(no_xgmi=False), bench.CONFIGS["c2"], _FakePkg())
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["n_gpus"] == 4 and line["value"] > 0  # the headline is there
@@ -303,6 +304,18 @@ def test_xgmi_probe_parts_link_rates_and_timeouts(monkeypatch, capsys):
     assert r["busbw_GBps"] == pytest.approx(41.9, abs=0.01) and r["frac_of_link"] == pytest.approx(41.9 / 153, abs=1e-3)
     assert x["resident_ring"]["ch1_4194304"]["frac_of_link"] == pytest.approx(30 / 153, abs=1e-3)
     assert "timeout" in x["ring_processes_all_gpus"]["error"]
+
+
+def test_xgmi_probe_resident_parts_opt_in(monkeypatch):
+    """Without NEXR_XGMI_RESIDENT=1 the probe runs only row f4's parts (the peer step and the
+    host-sequenced process rings); the frozen device-resident ring is not launched across GPUs."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.delenv("NEXR_XGMI_RESIDENT", raising=False)
+    seen = []
+    monkeypatch.setattr(bench, "_bounded", lambda cmd, t: seen.append(cmd[2]) or {"gpus": [0, 1]})
+    res = bench.xgmi_probe()
+    assert seen == ["--peer-step", "--ring-only", "--ring-all"] and "resident_ring" not in res
 
 
 def test_xgmi_probe_skipped_on_one_gpu(monkeypatch):

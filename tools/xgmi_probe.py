@@ -88,6 +88,9 @@ def main(peer_step_only: bool = False) -> int:
                            "alg_GBps": round(3 * buf / t / 1e9, 1), "exact": bool(ok_write)}
     if not peer_step_only:
         out["ring_processes"] = ring_processes()
+        if os.environ.get("NEXR_XGMI_RESIDENT") != "1":
+            print(json.dumps(out), flush=True)
+            return 0
         try:
             out["resident_ring"] = resident_ring(min(n_dev, 8))
         except Exception as e:  # noqa: BLE001 - reported, never raised
@@ -130,7 +133,9 @@ def resident_ring(n_ranks: int, sizes=(1 << 22, 1 << 26, 1 << 28), channels=(1, 
     return out
 
 
-PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2, "simple_resident": 0}  # the last: nexrPeerRingAllReduceResident
+PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2}
+if os.environ.get("NEXR_XGMI_RESIDENT") == "1":  # frozen, beyond SURVEY §8: opt-in
+    PROTOCOLS["simple_resident"] = 0  # nexrPeerRingAllReduceResident
 LL_COUNT = 1 << 20  # the LL protocols run C1's 4 MiB only (they move 2x / 16/15x the payload)
 
 
@@ -198,8 +203,8 @@ def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "104
     r0 = lines[0]["results"]
     exact_all = all(v["exact"] for ln in lines for proto in ln["results"].values() for v in proto.values())
     return {"per_protocol_bytes": r0, "exact_all_ranks": exact_all, "gpus": [ln["gpu"] for ln in lines],
-            "ranks": f"{n_ranks} processes, rank r on GPU r, fp32 sum; SIMPLE (host-sequenced and device-resident) at "
-                     "4 and 64 MiB, LL and LL128 at 4 MiB; "
+            "ranks": f"{n_ranks} processes, rank r on GPU r, fp32 sum; SIMPLE at 4 and 64 MiB (and the "
+                     "device-resident form with NEXR_XGMI_RESIDENT=1), LL and LL128 at 4 MiB; "
                      "timings of rank 0"}
 
 
