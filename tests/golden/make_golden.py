@@ -45,14 +45,29 @@ SUM, PROD, MINMAX, PREMULSUM, SUMPOSTDIV = 0, 1, 2, 3, 4
 M64 = (1 << 64) - 1
 
 
-def splitmix64(seed: int, n: int) -> np.ndarray:
-    """n outputs of splitmix64 starting from `seed` (vectorised, wrapping uint64 arithmetic)."""
+def _splitmix64_into(z: np.ndarray, seed: int, first: int, tmp: np.ndarray) -> None:
+    """z[j] = output first + j of splitmix64 from `seed`, computed in place (wrapping uint64)."""
+    gamma, c1, c2 = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
     with np.errstate(over="ignore"):
-        i = np.arange(1, n + 1, dtype=np.uint64)
-        z = (np.uint64(seed & M64) + i * np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
+        z[:] = np.arange(first + 1, first + 1 + z.size, dtype=np.uint64)
+        np.multiply(z, gamma, out=z)
+        np.add(z, np.uint64(seed & M64), out=z)
+        for shift, mul in ((30, c1), (27, c2), (31, None)):
+            np.right_shift(z, np.uint64(shift), out=tmp)
+            np.bitwise_xor(z, tmp, out=z)
+            if mul is not None:
+                np.multiply(z, mul, out=z)
+
+
+def splitmix64(seed: int, n: int, chunk: int = 1 << 18) -> np.ndarray:
+    """n outputs of splitmix64 starting from `seed` (vectorised, wrapping uint64 arithmetic), in
+    cache-sized chunks with in-place steps."""
+    out = np.empty(n, dtype=np.uint64)
+    tmp = np.empty(min(n, chunk), dtype=np.uint64)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        _splitmix64_into(out[a:b], seed, a, tmp[:b - a])
+    return out
 
 
 def f32_to_f16_bits(x: np.ndarray) -> np.ndarray:
@@ -83,45 +98,81 @@ SPECIAL_F32 = np.array([np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-45, -1e-45, 1.175
                         1.005859375, 0.5, -2.0, 3.0], dtype=np.float32)
 
 
+def _gen_chunk(dt: int, r: np.ndarray, special: bool) -> np.ndarray:
+    """One stretch of an input buffer from its splitmix64 outputs `r` (every element depends only
+    on its own r[i], so any split into stretches gives the same buffer)."""
+    if dt in INTS:
+        a = r.astype(STORE[dt])  # full-range uniform bits (truncating cast)
+        if special:
+            bits = np.dtype(STORE[dt]).itemsize * 8
+            ext = np.array([0, 1, (1 << bits) - 1, 1 << (bits - 1), (1 << (bits - 1)) - 1, 2, 3],
+                           dtype=np.uint64).astype(STORE[dt])
+            pick = (r >> np.uint64(59)) < np.uint64(6)
+            a[pick] = ext[(r[pick] >> np.uint64(8)) % np.uint64(len(ext))]
+        return a
+    # uniform [-1, 1); r >> 40 < 2^24, so the int64 view converts exactly (and faster than uint64)
+    u = ((r >> np.uint64(40)).view(np.int64).astype(np.float64) * 2.0 ** -24 * 2.0 - 1.0)
+    f = u.astype(np.float32)
+    if special:
+        pick = (r >> np.uint64(58)) < np.uint64(10)
+        f[pick] = SPECIAL_F32[((r[pick] >> np.uint64(8)) % np.uint64(len(SPECIAL_F32))).astype(np.int64)]
+    if dt == F32:
+        return f
+    if dt == F64:
+        a = u.copy()
+        if special:
+            a[pick] = f[pick].astype(np.float64)
+        return a
+    if dt == F16:
+        a = f32_to_f16_bits(f)
+        raw = np.array([0x7E01, 0xFC00, 0x0001, 0x8001, 0x03FF, 0x7BFF, 0x3C00], dtype=np.uint16)
+    else:  # BF16
+        a = f32_to_bf16_bits(f)
+        raw = np.array([0x7FC1, 0xFF80, 0x0001, 0x8001, 0x7F7F, 0x3F80, 0x3BC0], dtype=np.uint16)
+    if special:  # raw 16-bit specials incl. NaN payloads and subnormals
+        p2 = (r >> np.uint64(61)) == np.uint64(0)
+        a[p2] = raw[((r[p2] >> np.uint64(16)) % np.uint64(len(raw))).astype(np.int64)]
+    return a
+
+
+GEN_CHUNK = 1 << 18
+
+
 def gen_inputs(dt: int, k: int, n: int, seed: int, special: bool) -> list:
-    """K input buffers (storage dtype) for one case; buffer s uses seed + s."""
+    """K input buffers (storage dtype) for one case; buffer s uses seed + s.
+    Large buffers are built in stretches of GEN_CHUNK elements on a thread pool (numpy releases the
+    GIL in its loops; every element depends only on its own splitmix64 output, so the bytes are the
+    same as one whole-buffer pass): the GPU suite's 100+ MiB buffers in seconds, not minutes."""
     out = []
     for s in range(k):
-        r = splitmix64(seed + s, n)
-        if dt in INTS:
-            a = r.astype(STORE[dt])  # full-range uniform bits (truncating cast)
-            if special:
-                bits = np.dtype(STORE[dt]).itemsize * 8
-                ext = np.array([0, 1, (1 << bits) - 1, 1 << (bits - 1), (1 << (bits - 1)) - 1, 2, 3],
-                               dtype=np.uint64).astype(STORE[dt])
-                pick = (r >> np.uint64(59)) < np.uint64(6)
-                a[pick] = ext[(r[pick] >> np.uint64(8)) % np.uint64(len(ext))]
+        a = np.empty(n, dtype=STORE[dt])
+
+        def fill(lo, s=s, a=a):
+            hi = min(n, lo + GEN_CHUNK)
+            r = np.empty(hi - lo, dtype=np.uint64)
+            _splitmix64_into(r, seed + s, lo, np.empty_like(r))
+            a[lo:hi] = _gen_chunk(dt, r, special)
+
+        starts = range(0, n, GEN_CHUNK)
+        if n <= 4 * GEN_CHUNK:
+            for lo in starts:
+                fill(lo)
         else:
-            u = ((r >> np.uint64(40)).astype(np.float64) * 2.0 ** -24 * 2.0 - 1.0)  # uniform [-1, 1)
-            f = u.astype(np.float32)
-            if special:
-                pick = (r >> np.uint64(58)) < np.uint64(10)
-                f[pick] = SPECIAL_F32[((r[pick] >> np.uint64(8)) % np.uint64(len(SPECIAL_F32))).astype(np.int64)]
-            if dt == F32:
-                a = f
-            elif dt == F64:
-                a = u.copy()
-                if special:
-                    a[pick] = f[pick].astype(np.float64)
-            elif dt == F16:
-                a = f32_to_f16_bits(f)
-                if special:  # raw half specials incl. NaN payloads and subnormals
-                    raw = np.array([0x7E01, 0xFC00, 0x0001, 0x8001, 0x03FF, 0x7BFF, 0x3C00], dtype=np.uint16)
-                    p2 = (r >> np.uint64(61)) == np.uint64(0)
-                    a[p2] = raw[((r[p2] >> np.uint64(16)) % np.uint64(len(raw))).astype(np.int64)]
-            else:  # BF16
-                a = f32_to_bf16_bits(f)
-                if special:
-                    raw = np.array([0x7FC1, 0xFF80, 0x0001, 0x8001, 0x7F7F, 0x3F80, 0x3BC0], dtype=np.uint16)
-                    p2 = (r >> np.uint64(61)) == np.uint64(0)
-                    a[p2] = raw[((r[p2] >> np.uint64(16)) % np.uint64(len(raw))).astype(np.int64)]
-        out.append(np.ascontiguousarray(a))
+            for _ in _pool().map(fill, starts):
+                pass
+        out.append(a)
     return out
+
+
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
+    return _POOL
 
 
 # ---- the independent restatement --------------------------------------------------------------
