@@ -1,5 +1,6 @@
 #!/bin/bash
-# Runs GPU steps one after another on the gpurun box: each line of the step file is
+# Runs GPU steps one after another on the gpurun box (step files under tools/steps/ are per-call
+# scratch, kept out of git; what they produced is under profiles/): each line of the step file is
 # "<seconds> <output file under gpurun_out/> <command...>". A step that fails ordinarily (exit 1-2,
 # e.g. a failing test) does not stop the next one; a time limit (124/137), an abort (134) or a
 # segmentation fault (139) ends the session there, as gpurun's rules require.
