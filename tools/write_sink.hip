@@ -1,16 +1,16 @@
 // Where does the write stream's cost arise? (diagnostic for DESIGN §6: 8 read streams alone stream at
-// ~6.8 TB/s, with one write stream beside them at ~6.05.) S read streams (fold = xor), then the
-// write stream in one of four forms:
-//   none      no store (the fold is kept live by a never-taken store)
-//   hbm       the reduce-copy's store: pack i to out + 16 i (256 MiB, written to HBM)
-//   cached    the same store instructions, addresses folded into an 8 MiB window (out + 16 (i mod
-//             2^19)): the bytes stay in the L2s / Infinity Cache and almost none reach HBM, while the
-//             store traffic from the CUs through the L2 is unchanged
-//   half_hbm  every second wave-instruction's store to HBM, the others into the 8 MiB window
-// If `cached` runs as fast as `none`, the penalty sits where the written bytes reach HBM (DRAM
-// scheduling); if it runs as slow as `hbm`, it sits on the chip's write path. Reads are the production
-// kernel's (nt, 16 B per lane, one-shot grid of 256 x 4 packs); median of blocks of 10 launches over 3
-// rotating buffer sets. Tuning harness, not product code.
+// ~6.6-6.8 TB/s, with one write stream beside them at ~5.9-6.05.) S read streams (fold = xor), then the
+// write stream in one of these forms:
+//   none        no store (the fold is kept live by a never-taken store)
+//   hbm         the reduce-copy's store: pack i to out + 16 i (256 MiB, written to HBM), nt
+//   win 512K    the same store instructions, addresses folded into a 512 KiB window (out + 16 (i mod
+//               2^15), plain stores): the lines stay dirty in each XCD's 4 MiB L2 and almost nothing
+//               leaves the XCD — the cost of the stores up to the L2
+//   win 64M     a 64 MiB window: more than an L2, less than the 256 MiB Infinity Cache — the lines are
+//               written back across the fabric into the memory-side cache but (mostly) not to DRAM
+//   half_hbm    every second wave-instruction's store to HBM (nt), the others into the 512 KiB window
+// Reads are the production kernel's (nt, 16 B per lane, one-shot grid of 256 x 4 packs); median of
+// blocks of 10 launches over 3 rotating buffer sets. Tuning harness, not product code.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DNEXR_DT=7 tools/write_sink.hip -o tools/write_sink
 #include "../nex-nccl_amd/csrc/nexr_kernels.hip"
 
@@ -31,8 +31,8 @@ using namespace nexr;
 struct Srcs {
   const char* p[8];
 };
-enum { kNone = 0, kHbm = 1, kCached = 2, kHalf = 3 };
-constexpr size_t kWindowPacks = (size_t)1 << 19;  // 8 MiB
+// MODE: 0 none, 1 hbm, 2 half_hbm, >= 8: window of 2^MODE packs
+enum { kNone = 0, kHbm = 1, kHalf = 2, kWinL2 = 15, kWinMall = 22 };
 
 template <int S, int MODE>
 __global__ __launch_bounds__(256) void k_sink(Srcs s, char* o, size_t nPacks) {
@@ -54,11 +54,11 @@ __global__ __launch_bounds__(256) void k_sink(Srcs s, char* o, size_t nPacks) {
       if (a.x == 0x9e3779b9u && a.y == 1u) *(u32x4*)o = a;
     } else if constexpr (MODE == kHbm) {
       st16<kPolNt>(o + j * 16, a);
-    } else if constexpr (MODE == kCached) {
-      st16<kPolPlain>(o + (j % kWindowPacks) * 16, a);
-    } else {
-      if (u & 1) st16<kPolPlain>(o + (j % kWindowPacks) * 16, a);
+    } else if constexpr (MODE == kHalf) {
+      if (u & 1) st16<kPolPlain>(o + (j & ((1ull << kWinL2) - 1)) * 16, a);
       else st16<kPolNt>(o + j * 16, a);
+    } else {
+      st16<kPolPlain>(o + (j & ((1ull << MODE) - 1)) * 16, a);
     }
   }
 }
@@ -88,14 +88,14 @@ int main(int argc, char** argv) {
     void (*fn)(Srcs, char*, size_t);
     std::vector<float> ms;
   };
-  std::vector<Case> cs = {
-      {"2R none", 2, kNone, k_sink<2, kNone>, {}},       {"2R + W hbm", 2, kHbm, k_sink<2, kHbm>, {}},
-      {"2R + W cached", 2, kCached, k_sink<2, kCached>, {}}, {"2R + W half_hbm", 2, kHalf, k_sink<2, kHalf>, {}},
-      {"4R none", 4, kNone, k_sink<4, kNone>, {}},       {"4R + W hbm", 4, kHbm, k_sink<4, kHbm>, {}},
-      {"4R + W cached", 4, kCached, k_sink<4, kCached>, {}}, {"4R + W half_hbm", 4, kHalf, k_sink<4, kHalf>, {}},
-      {"8R none", 8, kNone, k_sink<8, kNone>, {}},       {"8R + W hbm", 8, kHbm, k_sink<8, kHbm>, {}},
-      {"8R + W cached", 8, kCached, k_sink<8, kCached>, {}}, {"8R + W half_hbm", 8, kHalf, k_sink<8, kHalf>, {}},
-  };
+  std::vector<Case> cs;
+#define CASES(S)                                                           \
+  cs.push_back({#S "R none", S, kNone, k_sink<S, kNone>, {}});             \
+  cs.push_back({#S "R + W hbm", S, kHbm, k_sink<S, kHbm>, {}});            \
+  cs.push_back({#S "R + W win 512K", S, kWinL2, k_sink<S, kWinL2>, {}});   \
+  cs.push_back({#S "R + W win 64M", S, kWinMall, k_sink<S, kWinMall>, {}}); \
+  cs.push_back({#S "R + W half_hbm", S, kHalf, k_sink<S, kHalf>, {}});
+  CASES(2) CASES(4) CASES(8)
   for (auto& c : cs)
     for (int w = 0; w < 2; w++) c.fn<<<grid, 256>>>(ss[w % R], outs[w % R], P);
   CK(hipDeviceSynchronize());
