@@ -154,6 +154,7 @@ struct nexrRingComm {
   std::vector<int> devices;
   std::vector<hipStream_t> streams, streams2;  // streams2: the tree's broadcast-half threads
   std::vector<uint32_t*> status, status2;      // LL: pinned status words the kernel reports timeouts in
+  std::vector<uint32_t*> done, done2;          // per stream: pinned step-completion words (Prims::streamDone)
   bool ll = false;     // LL or LL128: one FIFO step per primitive call, data readiness in line flags
   int proto = nexrRingProtoSimple;
   bool needHip = false;
@@ -222,6 +223,7 @@ struct Prims {
   nexrReduceCopyLL128Fn ll128Fn;
   uint32_t* status;
   hipStream_t stream;
+  uint32_t* done = nullptr;  // the stream's completion word: [0] written by the GPU, [1] last ticket
   bool device;
   int proto = nexrRingProtoSimple;  // the communicator's, or LL for a small P2P message (sendrecv.h)
 
@@ -242,6 +244,41 @@ struct Prims {
       recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
     }
     for (int i = 0; i < nSend; i++) send[i]->sendStep = (send[i]->sendStep + cs - 1) / cs * cs;
+  }
+
+  // The step queued on `stream` is complete (its bytes are in place before postPeer publishes them,
+  // prims_simple.h:177-188). A hipStreamWriteValue32 of a fresh ticket into the stream's pinned,
+  // device-mapped word follows the step, and the thread spins on the word: the command processor
+  // writes it only after the step's kernel has finished, end-of-kernel release included, so the next
+  // rank's launch sees the bytes exactly as after hipStreamSynchronize — 2.6-2.8 us cheaper per step
+  // on MI355X (tools/step_sync_probe.cpp, profiles/r03y_step_sync.txt). Without a word, if the write
+  // cannot be queued, or after the communicator's timeout, it falls back to hipStreamSynchronize (so
+  // it never returns with the step still in flight). NEXR_STEP_WAIT=word selects it (default: sync).
+  bool streamDone() {
+    if (done && stepWaitByWord()) {
+      const uint32_t t = ++done[1];
+      if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
+        const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+        auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spins = 0;; spins++) {
+          if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == t) return true;
+          if (spins >= 4096) {
+            if ((spins & 255) == 0 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs))
+              break;
+            std::this_thread::yield();
+          }
+        }
+      }
+    }
+    return hipStreamSynchronize(stream) == hipSuccess;
+  }
+  static bool stepWaitByWord() {
+    static const bool on = [] {
+      const char* e = getenv("NEXR_STEP_WAIT");
+      return e && !strcmp(e, "word");
+    }();
+    return on;
   }
 
   // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
@@ -301,8 +338,7 @@ struct Prims {
         nexrResult_t r = fn(k, srcs, m, dsts, (size_t)sliceSize, datatype, devOp, redOpArgs[0], nPre,
                             nPre ? redOpArgs : nullptr, postOp ? 1 : 0, (nexrStream_t)stream);
         if (r == nexrSuccess && device) {
-          hipError_t e = hipStreamSynchronize(stream);  // data complete before the step is posted
-          if (e != hipSuccess) r = nexrUnhandledCudaError;
+          if (!streamDone()) r = nexrUnhandledCudaError;  // data complete before the step is posted
         }
         if (r != nexrSuccess) {
           sh->fail(r);
@@ -365,7 +401,7 @@ struct Prims {
       else
         r = llFn(src, srcIsInput, nr, recvLines, rf32, dst, ns, sendLines, sf32, (size_t)nelem, datatype, devOp,
                  redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
-      if (r == nexrSuccess && device && hipStreamSynchronize(stream) != hipSuccess) r = nexrUnhandledCudaError;
+      if (r == nexrSuccess && device && !streamDone()) r = nexrUnhandledCudaError;
       if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
       if (r != nexrSuccess) {
         sh->fail(r);

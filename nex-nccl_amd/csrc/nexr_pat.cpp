@@ -489,7 +489,7 @@ struct PatRank {
       if (op.postRecv && op.recvDim >= 0) postRecv[op.recvDim] = true;
       if (op.postSend && op.sendDim >= 0) postSend[op.sendDim] = true;
     }
-    if (p.device && hipStreamSynchronize(p.stream) != hipSuccess) {
+    if (p.device && !p.streamDone()) {
       p.sh->fail(nexrUnhandledCudaError);
       return false;
     }

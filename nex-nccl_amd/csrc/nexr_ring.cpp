@@ -318,6 +318,27 @@ nexrResult_t defaultDeviceFn(int nSrcs, const void* const* srcs, int nDsts, void
   return nexrReduceCopy(nSrcs, srcs, nDsts, dsts, n, dt, op, arg, nPre, pre, post, s);
 }
 
+// The pinned, device-mapped completion word of one stream (Prims::streamDone): [0] is written by
+// the stream's hipStreamWriteValue32, [1] holds the last ticket handed out.
+nexrResult_t allocDone(uint32_t** w) {
+  if (hipHostMalloc((void**)w, 2 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+    *w = nullptr;
+    return nexrUnhandledCudaError;
+  }
+  (*w)[0] = (*w)[1] = 0;
+  return nexrSuccess;
+}
+
+// The completion word of `stream` (one of the communicator's streams), or nullptr.
+uint32_t* doneFor(const nexrRingComm* c, hipStream_t stream) {
+  if (!stream) return nullptr;
+  for (size_t r = 0; r < c->streams.size() && r < c->done.size(); r++)
+    if (c->streams[r] == stream) return c->done[r];
+  for (size_t r = 0; r < c->streams2.size() && r < c->done2.size(); r++)
+    if (c->streams2[r] == stream) return c->done2[r];
+  return nullptr;
+}
+
 Prims makePrims(nexrRingComm* c, Shared* sh, int rank, const void* sendbuff, void* recvbuff, size_t esz, int datatype,
                 const nexrDevRedOpFull& red, Geom g, hipStream_t stream, uint32_t* status) {
   Prims p;
@@ -338,6 +359,7 @@ Prims makePrims(nexrRingComm* c, Shared* sh, int rank, const void* sendbuff, voi
   p.ll128Fn = c->cfg.ll128Fn;
   p.status = status;
   p.stream = stream;
+  p.done = doneFor(c, stream);
   p.device = c->cfg.memMode == nexrRingDeviceMemory;
   p.proto = c->proto;
   return p;
@@ -466,10 +488,12 @@ nexrResult_t ensureSecondStreams(nexrRingComm* c) {
   const int n = c->cfg.nRanks;
   c->streams2.assign(n, nullptr);
   c->status2.assign(n, nullptr);
+  c->done2.assign(n, nullptr);
   for (int r = 0; r < n; r++) {
     if (c->streams[r]) {
       if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams2[r]) != hipSuccess)
         return nexrUnhandledCudaError;
+      if (allocDone(&c->done2[r]) != nexrSuccess) return nexrUnhandledCudaError;
     }
     if (c->ll) {
       nexrResult_t res = allocStatus(c, &c->status2[r]);
@@ -1313,6 +1337,7 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   c->devices.assign(n, 0);
   c->streams.assign(n, nullptr);
   c->status.assign(n, nullptr);
+  c->done.assign(n, nullptr);
   int nDev = 0;
   c->needHip = needsHip(*cfg);
   c->pinnedStatus = c->needHip;
@@ -1326,7 +1351,8 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   for (int r = 0; r < n; r++) {
     c->conns.push_back(new Conn());
     if (nDev > 0) {
-      if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams[r]) != hipSuccess) {
+      if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams[r]) != hipSuccess ||
+          allocDone(&c->done[r]) != nexrSuccess) {
         nexrRingCommDestroy(c);
         return nexrUnhandledCudaError;
       }
@@ -1524,6 +1550,9 @@ NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t c) {
         (void)hipSetDevice(c->devices[r]);
         (void)hipStreamDestroy((*v)[r]);
       }
+  for (auto* v : {&c->done, &c->done2})
+    for (uint32_t* w : *v)
+      if (w) (void)hipHostFree(w);
   delete c;
   return nexrSuccess;
 }
@@ -1572,6 +1601,7 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   c->devices.assign(n, cfg->device);
   c->streams.assign(n, nullptr);
   c->status.assign(n, nullptr);
+  c->done.assign(n, nullptr);
   c->pinnedStatus = true;
   for (int r = 0; r < n; r++) {
     c->conns.push_back(new Conn());
@@ -1583,7 +1613,8 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
     nexrRingCommDestroy(c);
     return r;
   };
-  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreate(&c->streams[me]) != hipSuccess)
+  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreate(&c->streams[me]) != hipSuccess ||
+      allocDone(&c->done[me]) != nexrSuccess)
     return fail(nexrUnhandledCudaError);
   if (c->ll && allocStatus(c, &c->status[me]) != nexrSuccess) return fail(nexrUnhandledCudaError);
   // The FIFO into this rank. Uncached device memory: it is written by another process's kernels
