@@ -253,7 +253,7 @@ struct Prims {
   // rank's launch sees the bytes exactly as after hipStreamSynchronize — 2.6-2.8 us cheaper per step
   // on MI355X (tools/step_sync_probe.cpp, profiles/r03y_step_sync.txt). Without a word, if the write
   // cannot be queued, or after the communicator's timeout, it falls back to hipStreamSynchronize (so
-  // it never returns with the step still in flight). NEXR_STEP_WAIT=word selects it (default: sync).
+  // it never returns with the step still in flight). NEXR_STEP_WAIT=sync selects the plain wait.
   bool streamDone() {
     if (done && stepWaitByWord()) {
       const uint32_t t = ++done[1];
@@ -276,7 +276,7 @@ struct Prims {
   static bool stepWaitByWord() {
     static const bool on = [] {
       const char* e = getenv("NEXR_STEP_WAIT");
-      return e && !strcmp(e, "word");
+      return !(e && !strcmp(e, "sync"));
     }();
     return on;
   }
