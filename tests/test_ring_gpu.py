@@ -86,3 +86,42 @@ def test_ll128_ring_device_memory(ring, oracle, n_ranks, dt, op):
     exp = ring_allreduce_expected_ll(inputs, dt, op, 120 * 640 * 8 * 8, proto="ll128")
     for r in range(n_ranks):
         assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"rank {r}"
+
+
+_STEP_WAIT_SCRIPT = r"""
+import importlib, json, sys
+sys.path.insert(0, {root!r})
+import numpy as np, torch
+ring = importlib.import_module("nex-nccl_amd.ring")
+n, count, ok = 3, 200_003, True
+rng = np.random.default_rng(5)
+# small integers: every fold order gives the same fp32 sums, so the result is checked exactly
+x = [rng.integers(-1000, 1000, count).astype(np.float32) for _ in range(n)]
+exp = x[0] + x[1] + x[2]
+send = [torch.from_numpy(v).cuda() for v in x]
+for proto in (ring.PROTO_SIMPLE, ring.PROTO_LL, ring.PROTO_LL128):
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 0, protocol=proto) as comm:
+        for call in (comm.all_reduce, comm.tree_all_reduce, comm.all_reduce):
+            recv = [torch.zeros_like(t) for t in send]
+            torch.cuda.synchronize()
+            call([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, 7, 0)
+            ok = ok and all(np.array_equal(r.cpu().numpy(), exp) for r in recv)
+print(json.dumps({{"ok": bool(ok)}}))
+"""
+
+
+@pytest.mark.parametrize("wait", ["sync", "word"])
+def test_step_wait_modes_give_the_same_results(wait):
+    """NEXR_STEP_WAIT (read once per process): the completion-word wait (default) and the plain
+    hipStreamSynchronize wait run the ring, tree and ring all-reduces again with every protocol on one
+    communicator, in a fresh process each, and every rank of every call holds the exact sums."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = _STEP_WAIT_SCRIPT.format(root=root)
+    env = dict(os.environ, NEXR_STEP_WAIT=wait)
+    out = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])["ok"]
