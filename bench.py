@@ -16,8 +16,8 @@ Either N > 1 way also times an N=1 leg on GPU 0 in the same run, and every GPU a
 them beside the aggregate under `c5`.
 
 Prints ONE JSON line on rank 0 (keys per the driver contract, plus `roofline`, `cpu_baseline`,
-`h2d_inclusive`, `extra_configs` / `c1_ring` / `resident_ring` at N=1 and `per_gpu` / `c5` /
-`xgmi_probe` at N>1).
+`h2d_inclusive`, `extra_configs` / `c1_ring` at N=1 and `per_gpu` / `c5` / `xgmi_probe` /
+`phase_s` at N>1).
 """
 from __future__ import annotations
 
@@ -29,6 +29,7 @@ import os
 import sys
 import time
 
+_T0 = time.perf_counter()  # process start (before torch): every N > 1 line reports its phases from here
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -379,7 +380,6 @@ def c1_ring(iters: int = 20) -> dict:
     cpu_fn = ctypes.cast(ol.oracle_reduce_copy_emulated_fn, ctypes.c_void_p).value
     out = {"workload": "fp32 sum all-reduce, 4 MiB per rank, 2 emulated ranks, ring SIMPLE, 1 channel"}
     legs = (("device", ring.DEVICE_MEMORY, None, ring.PROTO_SIMPLE),
-            ("device_resident", ring.DEVICE_MEMORY, None, ring.PROTO_SIMPLE),
             ("device_ll", ring.DEVICE_MEMORY, None, ring.PROTO_LL),
             ("device_ll128", ring.DEVICE_MEMORY, None, ring.PROTO_LL128),
             ("host_staged", ring.HOST_MEMORY, None, ring.PROTO_SIMPLE),
@@ -398,50 +398,22 @@ def c1_ring(iters: int = 20) -> dict:
         rp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in recv]
         reps = iters if fn is None else max(2, iters // 10)
         with ring.RingComm(n, mode, 0, fn, protocol=proto, timeout_ms=10000) as comm:
-            call = comm.all_reduce_resident if name == "device_resident" else comm.all_reduce
-            call(sp, rp, count, 7, 0)
+            wait = comm.step_wait()
+            comm.all_reduce(sp, rp, count, 7, 0)
             t0 = time.perf_counter()
             for _ in range(reps):
-                call(sp, rp, count, 7, 0)
+                comm.all_reduce(sp, rp, count, 7, 0)
             dt = (time.perf_counter() - t0) / reps
         got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
         out[name] = {"ms_per_call": round(dt * 1e3, 3), "algbw_gbs": round(count * 4 / dt / 1e9, 2), "calls": reps,
                      "exact": all(np.array_equal(g, expect) for g in got)}
-    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_resident runs the same schedule as one "
-                   "device-resident launch (nexrRingAllReduceResident: every rank's runRing inside the kernel, step "
-                   "counters in HBM) instead of one reduce-copy launch per slice; device_ll / device_ll128 run the same ring "
+        if mode == ring.DEVICE_MEMORY:
+            out[name]["step_wait"] = wait  # "word" with both ranks on one GPU, "sync" across GPUs
+    out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_ll / device_ll128 run the same ring "
                    "with the LL / LL128 protocol steps (SURVEY §8(f) #3) in place of SIMPLE; cpu_oracle runs the same schedule with the "
                    "reference's CPU execution of reduceCopy (oracle_reduce_copy_emulated_fn: 480 emulated threads, "
                    "Unroll 4) as its reduce-copy on host cores")
     return out
-
-
-def resident_ring(n: int = 2, nbytes: int = 256 << 20, channels: int = 4, iters: int = 10) -> dict:
-    """The ring all-reduce as one device-resident launch (nexrRingAllReduceResident) at a
-    bandwidth size: n emulated ranks on this GPU, fp32 sum of integer-valued inputs (exact check),
-    4 MiB buffers, `channels` channels. bytes_moved_rate counts every byte the schedule reads and
-    writes, S x (6n - 4) per call, FIFO bytes included (they may be Infinity-Cache-served)."""
-    import torch
-    ring = importlib.import_module("nex-nccl_amd.ring")
-    count = nbytes // 4
-    dev = torch.device("cuda", local_device_index())
-    xs = [torch.arange(count, dtype=torch.float32, device=dev).remainder_(1000) + r for r in range(n)]
-    ys = [torch.empty_like(x) for x in xs]
-    torch.cuda.synchronize(dev)
-    sp, rp = [x.data_ptr() for x in xs], [y.data_ptr() for y in ys]
-    with torch.cuda.device(dev), ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=channels,
-                                               timeout_ms=10000) as comm:
-        comm.all_reduce_resident(sp, rp, count, 7, 0)
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            comm.all_reduce_resident(sp, rp, count, 7, 0)
-        dt = (time.perf_counter() - t0) / iters
-    exp = torch.arange(count, dtype=torch.float32, device=dev).remainder_(1000) * n + n * (n - 1) // 2
-    exact = all(torch.equal(y, exp) for y in ys)
-    return {"workload": f"fp32 sum all-reduce, {nbytes >> 20} MiB per rank, {n} emulated ranks on one GPU, ring SIMPLE, "
-                        f"{channels} channels, one device-resident launch per call",
-            "ms_per_call": round(dt * 1e3, 4), "algbw_gbs": round(nbytes / dt / 1e9, 2),
-            "bytes_moved_rate_gbs": round(nbytes * (6 * n - 4) / dt / 1e9, 1), "calls": iters, "exact": bool(exact)}
 
 
 # ---- CPU baseline: the oracle (C restatement) on the benchmarked configuration ------------------
@@ -607,6 +579,26 @@ def _bounded(cmd, timeout_s: float):
 
 
 XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (MI355X_MICROARCH.md; 7 links per GPU)
+# Wall-time budget of an N > 1 line: the driver's BENCH timeout is 600 s; the whole line
+# (timed region, checks, solo legs, node-wide host rate, xGMI probe) is kept under TOTAL_CAP_S, and the
+# probe gets what is left of it, at most XGMI_BUDGET_S.
+TOTAL_CAP_S = 300.0
+XGMI_BUDGET_S = 180.0
+XGMI_MARGIN_S = 15.0
+# The probe's parts, in order, with their own limits (seconds). The process rings run twice, once with
+# every rank thread waiting for its steps by stream synchronisation (the cross-GPU default) and once
+# by the completion word (NEXR_STEP_WAIT=word): a mismatch under "word" alone is a step-visibility
+# fault, a mismatch under both a link or schedule fault.
+XGMI_PARTS = (("peer_step", ["--peer-step"], 45.0, 2),
+              ("ring_processes", ["--ring-only", "--step-wait", "sync"], 40.0, 2),
+              ("ring_processes_word", ["--ring-only", "--step-wait", "word"], 40.0, 2),
+              ("ring_processes_all_gpus", ["--ring-all", "{n}", "--step-wait", "sync"], 55.0, 3),
+              ("ring_processes_all_gpus_word", ["--ring-all", "{n}", "--step-wait", "word"], 55.0, 3))
+
+
+def probe_budget(elapsed_s: float) -> float:
+    """Seconds the xGMI probe may take after `elapsed_s` of the line: never past TOTAL_CAP_S."""
+    return max(0.0, min(XGMI_BUDGET_S, TOTAL_CAP_S - XGMI_MARGIN_S - elapsed_s))
 
 
 def xgmi_link_rates(res: dict) -> dict:
@@ -620,7 +612,7 @@ def xgmi_link_rates(res: dict) -> dict:
         if isinstance(v, dict) and "xgmi_GBps" in v:
             v["link_bound_GBps"] = XGMI_LINK_GBS
             v["frac_of_link"] = round(v["xgmi_GBps"] / XGMI_LINK_GBS, 4)
-    for key in ("ring_processes", "ring_processes_all_gpus"):
+    for key in ("ring_processes", "ring_processes_word", "ring_processes_all_gpus", "ring_processes_all_gpus_word"):
         v = res.get(key)
         if not isinstance(v, dict) or "per_protocol_bytes" not in v:
             continue
@@ -639,16 +631,39 @@ def xgmi_link_rates(res: dict) -> dict:
     return res
 
 
-def xgmi_probe(budget_s: float = 240.0):
+def step_wait_verdict(res: dict) -> dict:
+    """Both step waits side by side for each process ring that ran: exact on every rank under the
+    synchronisation and under the completion word, and what a difference means."""
+    out = {}
+    for key in ("ring_processes", "ring_processes_all_gpus"):
+        sync, word = res.get(key), res.get(key + "_word")
+        if not isinstance(sync, dict) and not isinstance(word, dict):
+            continue
+        ex = lambda v: v.get("exact_all_ranks") if isinstance(v, dict) else None  # noqa: E731
+        out[key] = {"sync_exact_all_ranks": ex(sync), "word_exact_all_ranks": ex(word),
+                    "sync_in_effect": (sync or {}).get("step_wait_in_effect"),
+                    "word_in_effect": (word or {}).get("step_wait_in_effect")}
+    sync_ok = [v["sync_exact_all_ranks"] for v in out.values()]
+    word_ok = [v["word_exact_all_ranks"] for v in out.values()]
+    out["visibility_fault"] = any(s is True and w is False for s, w in zip(sync_ok, word_ok))
+    out["link_or_schedule_fault"] = any(s is False for s in sync_ok)
+    out["note"] = ("the cross-GPU default is the synchronisation (nexrRingCommGetStepWait); a ring exact under "
+                   "sync but not under the word would be a step-visibility fault, not a link fault")
+    return out
+
+
+def xgmi_probe(budget_s: float = XGMI_BUDGET_S):
     """The peer-memory step over xGMI (tools/xgmi_probe.py), after the timed region, each part in a
     bounded subprocess of its own so one hang cannot cost the others or the line: GPU 0's kernel with
-    an operand in GPU 1's HBM, the two-rank process ring, the resident ring over all GPUs (only with
-    NEXR_XGMI_RESIDENT=1: frozen, beyond §8), and with three or more GPUs the process ring over all
-    of them (up to 8). The parts share `budget_s`; a part that times out is recorded as such.
+    an operand in GPU 1's HBM, the two-rank process ring under both step waits, and with three or more
+    GPUs the process ring over all of them (up to 8) under both step waits. With NEXR_XGMI_RESIDENT=1
+    and the opt-in extras library built, also the resident ring over all GPUs (beyond SURVEY §8). The
+    parts share `budget_s`; a part that times out or finds the budget spent is recorded as such.
     Reported, never allowed to fail the bench line."""
     import torch
     probe = os.path.join(ROOT, "tools", "xgmi_probe.py")
-    t_end = time.perf_counter() + budget_s
+    t0 = time.perf_counter()
+    t_end = t0 + budget_s
     n_dev = torch.cuda.device_count()
 
     def part(args, limit):
@@ -657,15 +672,32 @@ def xgmi_probe(budget_s: float = 240.0):
             return {"error": "skipped: the probe budget is spent"}
         return _bounded([sys.executable, probe] + args, min(limit, left))
 
-    res = part(["--peer-step"], 60.0)
+    res = None
+    part_s = {}
+    for key, args, limit, min_gpus in XGMI_PARTS:
+        if n_dev < min_gpus:
+            continue
+        t = time.perf_counter()
+        out = part([a.replace("{n}", str(min(n_dev, 8))) for a in args], limit)
+        part_s[key] = round(time.perf_counter() - t, 1)
+        if res is None:
+            res = out
+            if not isinstance(res, dict) or "skipped" in res:
+                break
+        else:
+            res[key] = out
+    if isinstance(res, dict) and "skipped" not in res and os.environ.get("NEXR_XGMI_RESIDENT") == "1":
+        t = time.perf_counter()
+        res["resident_ring"] = part(["--resident-only", str(min(n_dev, 8))], 60.0)
+        part_s["resident_ring"] = round(time.perf_counter() - t, 1)
+    if res is None:
+        res = {"skipped": f"needs 2 GPUs, found {n_dev}"}
     if isinstance(res, dict) and "skipped" not in res:
-        res["ring_processes"] = part(["--ring-only"], 75.0)
-        # The device-resident collectives go beyond SURVEY §8 and are frozen: their
-        # cross-GPU run is opt-in, so the default line spends its probe budget on row f4 only.
-        if os.environ.get("NEXR_XGMI_RESIDENT") == "1":
-            res["resident_ring"] = part(["--resident-only", str(min(n_dev, 8))], 60.0)
-        if n_dev >= 3:
-            res["ring_processes_all_gpus"] = part(["--ring-all", str(min(n_dev, 8))], 100.0)
+        res["step_wait_modes"] = step_wait_verdict(res)
+    if isinstance(res, dict):
+        res["budget_s"] = round(budget_s, 1)
+        res["part_s"] = part_s
+        res["wall_s"] = round(time.perf_counter() - t0, 1)
     return xgmi_link_rates(res)
 
 
@@ -802,6 +834,26 @@ def side_leg(fn, *a):
 
 
 # ---- the two ways to drive N GPUs ---------------------------------------------------------------
+class Phases:
+    """Wall seconds of each phase of a line since the process started (`phase_s`), so a line whose run
+    came close to the driver's timeout shows where the time went."""
+
+    def __init__(self):
+        self.t = time.perf_counter()
+        self.s = {"startup": round(self.t - _T0, 2)}
+
+    def mark(self, name: str) -> None:
+        now = time.perf_counter()
+        self.s[name] = round(now - self.t, 2)
+        self.t = now
+
+    def elapsed(self) -> float:
+        return time.perf_counter() - _T0
+
+    def summary(self) -> dict:
+        return dict(self.s, total=round(self.elapsed(), 2), cap_s=TOTAL_CAP_S)
+
+
 def main_ranks(args, cfg, pkg) -> dict | None:
     """One process per GPU (N=1 plain, or N>1 under torchrun): each rank times its own chunk."""
     import torch
@@ -812,8 +864,11 @@ def main_ranks(args, cfg, pkg) -> dict | None:
     dev_index = local_device_index()
     torch.cuda.set_device(dev_index)
     per_launch = args.events == "launch"
+    ph = Phases()
     wl = DeviceWorkload(pkg, cfg, dev_index, seed=1000 + dist.rank)
+    ph.mark("inputs")
     local_s, max_s, kernel_s = wl.run(args.steps, args.warmup, dist, per_launch)
+    ph.mark("timed_region")
     bytes_step = algorithmic_bytes(cfg)
     value = dist.world * bytes_step * args.steps / max_s / 1e9
     ranks = dist.gather([local_s, kernel_s], wl.dev)
@@ -822,6 +877,7 @@ def main_ranks(args, cfg, pkg) -> dict | None:
     exact = side_leg(wl.check_exact, wl.last_set)
     exact_ranks = [f[0] == 1.0 for f in dist.gather([1.0 if exact.get("exact") is True else 0.0], wl.dev)]
     sets = side_leg(wl.per_set) if dist.rank == 0 else None
+    ph.mark("exact_checks_and_per_set")
     c5 = None
     if dist.world > 1:
         # Same-run legs: rank 0's GPU alone (the N=1 reference), then every GPU alone in turn.
@@ -832,10 +888,12 @@ def main_ranks(args, cfg, pkg) -> dict | None:
             solo.append(dist.max(s, wl.dev))
             dist.barrier()
         c5 = c5_summary(dist.world, bytes_step, args.steps, max_s, solo[0], solo)
+        ph.mark("solo_legs")
     h2d_all = None
     if dist.world > 1 and not args.no_h2d:
         wl.free()
         h2d_all = h2d_pinned_all_ranks(pkg, cfg, dist, wl.dev)
+        ph.mark("h2d_all_ranks")
     result = None
     if dist.rank == 0:
         result = base_line(cfg, dist.world, args.steps, args.warmup, value, max_s,
@@ -854,7 +912,6 @@ def main_ranks(args, cfg, pkg) -> dict | None:
                 wl.free()
                 result["extra_configs"] = side_leg(extra_configs, pkg)
                 result["c1_ring"] = side_leg(c1_ring)
-                result["resident_ring"] = side_leg(resident_ring)
             if not args.no_cpu:
                 result["cpu_baseline"] = side_leg(cpu_baseline_entry, cfg, args.cpu_seconds)
             if not args.no_h2d:
@@ -864,7 +921,9 @@ def main_ranks(args, cfg, pkg) -> dict | None:
             result["c5"] = c5
             result["h2d_inclusive"] = h2d_all
             if not args.no_xgmi:
-                result["xgmi_probe"] = xgmi_probe()
+                result["xgmi_probe"] = xgmi_probe(probe_budget(ph.elapsed()))
+                ph.mark("xgmi_probe")
+            result["phase_s"] = ph.summary()
         print(json.dumps(result), flush=True)
     dist.barrier()
     dist.close()
@@ -884,6 +943,7 @@ def main_fanout(args, cfg, pkg) -> dict:
     if n_vis < args.gpus and not fold:
         raise SystemExit(f"--gpus {args.gpus} but only {n_vis} visible GPU(s)")
     devices = [d % n_vis for d in range(args.gpus)]
+    ph = Phases()
     # Three rotating buffer sets per GPU, as the N=1 line: launch k of a GPU runs set k mod 3
     # (nexrReduceCopyMultiDeviceSets), so no launch re-reads the previous one's cache-resident bytes.
     wls = [DeviceWorkload(pkg, cfg, dev, seed=1000 + d, sets=FANOUT_SETS) for d, dev in enumerate(devices)]
@@ -891,13 +951,16 @@ def main_fanout(args, cfg, pkg) -> dict:
         torch.cuda.synchronize(d)
     works = [[wl.work(s) for s in range(FANOUT_SETS)] for wl in wls]
     bytes_step = algorithmic_bytes(cfg)
+    ph.mark("inputs")
 
     def timed(ws, ds):
         pkg.reduce_copy_multi_device_sets(ws, ds, cfg["dt"], cfg["op"], reps=max(1, args.warmup))
         return pkg.reduce_copy_multi_device_sets(ws, ds, cfg["dt"], cfg["op"], reps=args.steps)
 
     agg_s = timed(works, devices)
+    ph.mark("timed_region")
     solo = [timed([works[i]], [devices[i]]) for i in range(args.gpus)]
+    ph.mark("solo_legs")
     value = args.gpus * bytes_step * args.steps / agg_s / 1e9
     result = base_line(cfg, args.gpus, args.steps, args.warmup, value, agg_s,
                        f"independent chunks x{args.gpus} (no collective), one process, "
@@ -909,6 +972,7 @@ def main_fanout(args, cfg, pkg) -> dict:
     result["exact_check"] = {"per_gpu": [c.get("exact") for c in checks],
                              "checked_elements_per_gpu": checks[0].get("checked_elements"),
                              "check": checks[0].get("check", checks[0].get("error"))}
+    ph.mark("exact_checks")
     # Roofline of the kernel itself: HIP events on GPU 0's launch stream, 3 rotating sets.
     for wl in wls:
         wl.free()
@@ -924,8 +988,11 @@ def main_fanout(args, cfg, pkg) -> dict:
     result["c5"]["timing"] = ("nexrReduceCopyMultiDeviceSets: barrier release to the last GPU's completion, "
                               f"{FANOUT_SETS} rotating buffer sets per GPU (as the N=1 line)")
     result["c5"]["sets_per_gpu"] = FANOUT_SETS
+    ph.mark("roofline_legs")
     if not args.no_xgmi:
-        result["xgmi_probe"] = xgmi_probe()
+        result["xgmi_probe"] = xgmi_probe(probe_budget(ph.elapsed()))
+        ph.mark("xgmi_probe")
+    result["phase_s"] = ph.summary()
     print(json.dumps(result), flush=True)
     return result
 

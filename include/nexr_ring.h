@@ -23,7 +23,11 @@
  *   - ncclLaunchOneRank for nRanks == 1 (src/device/onerank.cc:48-83),
  *   - op encoding through nexrHostToDevRedOp (src/enqueue.cc:2185-2278).
  * Every reduceCopy site calls a nexrReduceCopyFn — nexrReduceCopyHost (host memory) or
- * nexrReduceCopy + stream sync (device memory) by default.
+ * nexrReduceCopy + a wait for the step's completion (device memory) by default.
+ *
+ * Library: libnexr_ring.so (links libnexr.so). The schedules beyond SURVEY §8's rows — ncclSend /
+ * ncclRecv and the device-resident forms — are declared in nexr_extras.h and built only into the
+ * opt-in libnexr_extras.so (a superset of libnexr_ring.so; `make EXTRAS=1`).
  */
 #ifndef NEXR_RING_H_
 #define NEXR_RING_H_
@@ -77,7 +81,7 @@ typedef struct {
                            its own links, FIFOs, streams and host threads and they run concurrently.
                            Like the reference's duplicated channels (graph/connect.cc:146-160), the
                            upper half of 2 or more channels uses the other tree of the double binary
-                           tree. Send/Recv always uses channel 0 */
+                           tree. Send/Recv (extras) always uses channel 0 */
 } nexrRingConfig;
 
 typedef struct nexrRingComm* nexrRingComm_t;
@@ -89,36 +93,6 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* comm, const nexrRingCon
  * (host or device memory per memMode; in-place allowed). op is an ncclRedOp_t built-in. */
 NEXR_API nexrResult_t nexrRingAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op);
-
-/* ncclAllReduce (ring, SIMPLE) as ONE device-resident launch per GPU instead of one reduce-copy launch
- * per slice: every rank's runRing (all_reduce.h:12-84) runs inside the kernel, its blocks waiting on
- * step counters in HBM (waitPeer/postPeer, prims_simple.h:111-188) instead of the host sequencing
- * steps. Same arguments, chunking, channel split and per-element results as nexrRingAllReduce.
- * Requires memMode = device, protocol = SIMPLE, nRanks <= 16, and is nexrInvalidUsage under
- * nexrSemanticsShipped. Each (rank, channel) runs as a team of workgroups (NEXR_RESIDENT_TEAM, default
- * ~512 workgroups per GPU), each moving its own byte range of every FIFO slot with its own step
- * counters. A step wait that exceeds timeoutMs fails the call (nexrInternalError) and marks the
- * communicator broken. Blocks until every GPU's launch has finished. */
-NEXR_API nexrResult_t nexrRingAllReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
-                                                void* const* recvbuffs, size_t count, int datatype, int op);
-
-/* The other ring collectives the same way, arguments, results and restrictions as their host-sequenced
- * forms below and as nexrRingAllReduceResident: runRing of ReduceScatter (reduce_scatter.h:12-52),
- * AllGather (all_gather.h:12-66, in place when sendbuffs[r] == recvbuffs[r] + r*sendcount elements),
- * Reduce (reduce.h:12-50) and Broadcast (broadcast.h:12-58) inside one launch per GPU. */
-/* The tree ncclAllReduce (runTreeSplit, all_reduce.h:150-230) the same way: per (rank, channel) one team
- * reduces up and one broadcasts down, as the reference splits a block's threads; same topology,
- * chunking, results and restrictions as nexrTreeAllReduce / nexrRingAllReduceResident. */
-NEXR_API nexrResult_t nexrTreeAllReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
-                                                void* const* recvbuffs, size_t count, int datatype, int op);
-NEXR_API nexrResult_t nexrRingReduceScatterResident(nexrRingComm_t comm, const void* const* sendbuffs,
-                                                    void* const* recvbuffs, size_t recvcount, int datatype, int op);
-NEXR_API nexrResult_t nexrRingAllGatherResident(nexrRingComm_t comm, const void* const* sendbuffs,
-                                                void* const* recvbuffs, size_t sendcount, int datatype);
-NEXR_API nexrResult_t nexrRingReduceResident(nexrRingComm_t comm, const void* const* sendbuffs,
-                                             void* const* recvbuffs, size_t count, int datatype, int op, int root);
-NEXR_API nexrResult_t nexrRingBroadcastResident(nexrRingComm_t comm, const void* const* sendbuffs,
-                                                void* const* recvbuffs, size_t count, int datatype, int root);
 
 /* ncclReduceScatter: rank r's sendbuffs[r] holds nRanks*recvcount elements; recvbuffs[r] receives the
  * reduction of every rank's segment r (recvcount elements). */
@@ -144,44 +118,16 @@ NEXR_API nexrResult_t nexrRingBroadcast(nexrRingComm_t comm, const void* const* 
 NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
                                         size_t count, int datatype, int op);
 
-/* ncclReduceScatter / ncclAllGather with NCCL_ALGO_PAT, the Parallel Aggregated Trees schedules
- * (PatRSAlgorithm / PatAGAlgorithm, src/device/collectives.h:433-906; the worker loops of
- * reduce_scatter.h:80-139 and all_gather.h:113-172; patReduce / patCopy, prims_simple.h:992-1183).
- * Rank r exchanges with r -/+ 2^d for every d with 2^d < nRanks; the link r -> r+1 is the ring
- * connection, the others are made by the first PAT call. SIMPLE protocol only (nexrInvalidUsage
- * otherwise), and, as the reference's algorithm selection (src/enqueue.cc:1779-1780), no
- * ReduceScatter with ncclAvg (nexrInvalidArgument). Arguments as nexrRingReduceScatter /
- * nexrRingAllGather; in-place AllGather allowed. */
-NEXR_API nexrResult_t nexrPatReduceScatter(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
-                                           size_t recvcount, int datatype, int op);
-NEXR_API nexrResult_t nexrPatAllGather(nexrRingComm_t comm, const void* const* sendbuffs, void* const* recvbuffs,
-                                       size_t sendcount, int datatype);
-
-/* ncclSend / ncclRecv issued by every rank inside one ncclGroupStart/End (the P2P work batch,
- * src/device/sendrecv.h): rank r sends `bytes` bytes of sendbuffs[r] to rank sendPeers[r] and
- * receives `bytes` bytes from rank recvPeers[r] into recvbuffs[r] (-1: no send / no recv). Every
- * send must meet the matching recv (recvPeers[sendPeers[r]] == r), else nexrInvalidArgument. A
- * rank's send and recv run concurrently on its two streams over connection-index-1 FIFOs with
- * 8 steps of the P2P chunk size (128 KiB, at most buffBytes/8); a send to self is one copy.
- * Messages of at most 16 KiB move as LL lines (enqueue.cc:786-839) when the LL step can reach them
- * (device memory, or a caller-supplied llFn), else as SIMPLE chunks. The communicator's own protocol
- * must be SIMPLE (nexrInvalidUsage otherwise). */
-NEXR_API nexrResult_t nexrSendRecv(nexrRingComm_t comm, const void* const* sendbuffs, const int* sendPeers,
-                                   void* const* recvbuffs, const int* recvPeers, size_t bytes);
-
-/* The PAT step stream one rank's compute thread generates for a collective of `count` elements per
- * rank (recvcount for ReduceScatter, sendcount for AllGather), with the chunking of a communicator
- * whose SIMPLE buffer is buffBytes (0 = 4 MiB). Writes up to capOps steps to ops[12*i ..] as
- * {recvDim, sendDim, recvOffset, sendOffset, stepOffset, postRecv, postSend, nelem, last, skipped,
- * inpIx, outIx} (ncclPatStep, src/device/collectives.h:407-410), the total in *nOps and the worker
- * groups per batch in *parallelFactor. Host only: no communicator, no device. */
-NEXR_API nexrResult_t nexrPatSchedule(int reduceScatter, int nRanks, int rank, size_t count, int datatype,
-                                      size_t buffBytes, int64_t* ops, size_t capOps, size_t* nOps,
-                                      int* parallelFactor);
-
 /* The tree links of `rank` in this communicator's topology: *up (-1 at the root) and down[0..2]
  * (-1 when absent, children packed first as setTreeDown does). */
 NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t comm, int rank, int* up, int* down);
+
+/* How this communicator's rank threads wait for each device step before posting it (*word = 1: a
+ * hipStreamWriteValue32 completion word the thread spins on; 0: hipStreamSynchronize). The word is
+ * the default only when every rank runs on the same GPU; when the ranks span GPUs (thread ranks on
+ * several devices, or process ranks whose published GPUs differ) the default is the
+ * synchronisation. NEXR_STEP_WAIT=word / sync, read once per process, forces either. */
+NEXR_API nexrResult_t nexrRingCommGetStepWait(nexrRingComm_t comm, int* word);
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t comm);
 
@@ -211,32 +157,8 @@ typedef struct {
 NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* comm, const nexrPeerRingConfig* config);
 
 /* ncclAllReduce for this process's rank (sendbuff/recvbuff on config->device; in-place allowed). */
-/* PAT ReduceScatter / AllGather for this process's rank (arguments and restrictions as
- * nexrPatReduceScatter / nexrPatAllGather). The first PAT call on a communicator connects the
- * rank's r -/+ 2^d links through the shared segment (collective; up to 64 ranks). */
-NEXR_API nexrResult_t nexrPeerPatReduceScatter(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
-                                               size_t recvcount, int datatype, int op);
-NEXR_API nexrResult_t nexrPeerPatAllGather(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
-                                           size_t sendcount, int datatype);
-
-/* ncclSend / ncclRecv for this process's rank inside one group: send `bytes` of sendbuff to rank
- * sendPeer and receive `bytes` from recvPeer into recvbuff (-1: none; sendPeer == recvPeer == own rank
- * is a local copy). The send runs on a second thread beside the recv. The first call connects P2P
- * links to every rank (collective: all ranks make their first call together; up to 64 ranks);
- * afterwards every send must meet the matching recv on the peer in the same call. */
-NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t comm, const void* sendbuff, int sendPeer, void* recvbuff,
-                                       int recvPeer, size_t bytes);
-
 NEXR_API nexrResult_t nexrPeerRingAllReduce(nexrRingComm_t comm, const void* sendbuff, void* recvbuff, size_t count,
                                             int datatype, int op);
-
-/* The same all-reduce with this process's rank of the schedule inside one device-resident launch
- * (nexrRingAllReduceResident's kernel): the ranks' launches, each in its own process, meet only
- * through the FIFOs and the step records behind them, mapped over IPC. SIMPLE only, <= 16 ranks;
- * every rank makes the same calls. Blocks until this rank's launch has finished; a step wait past
- * timeoutMs returns nexrInternalError and aborts the communicator. */
-NEXR_API nexrResult_t nexrPeerRingAllReduceResident(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,
-                                                    size_t count, int datatype, int op);
 
 /* The other ring collectives for this process's rank, arguments as in the thread-rank versions. */
 NEXR_API nexrResult_t nexrPeerRingReduceScatter(nexrRingComm_t comm, const void* sendbuff, void* recvbuff,

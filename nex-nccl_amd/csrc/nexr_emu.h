@@ -1,6 +1,7 @@
-// nexr_emu.h — internal to the CPU-emulated collectives (nexr_ring.cpp, nexr_pat.cpp, nexr_p2p.cpp):
-// the connection and FIFO state, the communicator, and the host-side Primitives every schedule
-// drives. Not installed; the public surface is include/nexr_ring.h.
+// nexr_emu.h — internal to the CPU-emulated collectives (nexr_ring.cpp; the extras library's
+// nexr_p2p.cpp and nexr_resident_host.cpp): the connection and FIFO state, the communicator, and the
+// host-side Primitives every schedule drives. Not installed; the public surface is
+// include/nexr_ring.h (and include/nexr_extras.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
@@ -83,7 +84,6 @@ struct alignas(64) PeerHeader {
   std::atomic<uint32_t> joined;
   std::atomic<uint32_t> left;
   std::atomic<uint32_t> abort;
-  std::atomic<uint32_t> patJoined;  // ranks that published their PAT receive FIFOs
   std::atomic<uint32_t> p2pJoined;  // ranks that published their P2P receive FIFOs
   uint32_t magic, nRanks, protocol, pad;
   uint64_t buffBytes;
@@ -100,13 +100,14 @@ struct PeerSlot {
   std::atomic<uint64_t> residentGpu;
   std::atomic<int64_t> residentCap;   // workgroups per part rank r's GPU keeps resident
   std::atomic<int32_t> residentTeam;  // rank r's proposed team; 0 = not published yet
+  std::atomic<uint64_t> gpu;          // rank r's GPU (PCI domain/bus/device + 1), published when it joins
 };
-// Links beyond the ring for PAT (r -> r +- 2^d) and P2P (any r -> q), one per ordered pair: the
-// receiver's FIFO handles and the link's counters. Only for communicators of up to kPeerLinkMaxRanks.
+// Links beyond the ring for P2P (any r -> q, the extras library's send/recv), one per ordered pair:
+// the receiver's FIFO handles and the link's counters. Only for communicators of up to
+// kPeerLinkMaxRanks.
 constexpr int kPeerLinkMaxRanks = 64;
 struct PeerLink {
-  hipIpcMemHandle_t patFifo, p2pFifo, p2pLLFifo;
-  alignas(64) ConnState pat;
+  hipIpcMemHandle_t p2pFifo, p2pLLFifo;
   alignas(64) ConnState p2p;
   alignas(64) ConnState p2pLL;
 };
@@ -144,7 +145,6 @@ struct nexrRingComm {
   std::vector<TreeLinks> tree;  // tree topology (computed at creation)
   std::vector<Conn*> treeUp;    // treeUp[r]: r -> parent(r) (reduce); created by the first tree call
   std::vector<Conn*> treeDown;  // treeDown[r]: parent(r) -> r (broadcast)
-  std::vector<Conn*> patConns;  // PAT: patConns[from*nRanks+to] for to = from +- 2^d (ring link excluded)
   std::vector<Conn*> p2pConns;  // ncclSend/ncclRecv: p2pConns[from*nRanks+to] (connIndex 1), made on first use
   std::vector<Conn*> p2pLLConns;  // the same links' LL buffers, for messages <= 16 KiB
   // Channels 1..nChannels-1, each a communicator of its own (links, FIFOs, streams, tree) over the
@@ -160,6 +160,13 @@ struct nexrRingComm {
   bool needHip = false;
   bool pinnedStatus = false;  // status words from hipHostMalloc (else calloc)
   bool broken = false;
+  // How a rank thread waits for its step (Prims::streamDone): the completion word when every rank of
+  // the communicator runs on one GPU, hipStreamSynchronize when the ranks span GPUs (the step's stores
+  // then land in a peer GPU's memory, and only the synchronisation is documented to cover them).
+  // NEXR_STEP_WAIT=word / sync forces either (stepWaitMode).
+  bool stepWaitWord = true;
+  // Frees what the extras library attached to this communicator (set by its first resident call).
+  void (*freeExtras)(nexrRingComm*) = nullptr;
   // Resident ring (nexrRingAllReduceResident), made by its first call: for every device hosting ranks
   // (resDevs, in order of first appearance), the (channel, rank) connection table and the step-counter
   // block in that device's memory, and a pinned, device-mapped status word.
@@ -176,6 +183,7 @@ struct nexrRingComm {
   int ringLinkUser = 0;          // last user of the ring link r -> r+1: 0 none, 1 host-sequenced, 2 resident
   uint64_t residentCalls = 0;    // resident all-reduces this rank has completed
   int residentTeamAgreed = 0;    // process ranks: the team size all ranks agreed on (first resident call)
+  int residentSharing = 1;       // process ranks: ranks on this rank's GPU (published at that agreement)
   int self = 0;
   void* shm = nullptr;
   size_t shmBytes = 0;
@@ -247,15 +255,17 @@ struct Prims {
   }
 
   // The step queued on `stream` is complete (its bytes are in place before postPeer publishes them,
-  // prims_simple.h:177-188). A hipStreamWriteValue32 of a fresh ticket into the stream's pinned,
-  // device-mapped word follows the step, and the thread spins on the word: the command processor
-  // writes it only after the step's kernel has finished, end-of-kernel release included, so the next
-  // rank's launch sees the bytes exactly as after hipStreamSynchronize — 2.6-2.8 us cheaper per step
-  // on MI355X (tools/step_sync_probe.cpp, profiles/r03y_step_sync.txt). Without a word, if the write
-  // cannot be queued, or after the communicator's timeout, it falls back to hipStreamSynchronize (so
-  // it never returns with the step still in flight). NEXR_STEP_WAIT=sync selects the plain wait.
+  // prims_simple.h:177-188). Two ways to wait, chosen per communicator (stepWaitWord, below):
+  //   word: a hipStreamWriteValue32 of a fresh ticket into the stream's pinned, device-mapped word
+  //     follows the step, and the thread spins on the word. The command processor writes it only
+  //     after the step's kernel has finished, its end-of-kernel release included, so the next rank's
+  //     launch on the SAME GPU sees the bytes exactly as after hipStreamSynchronize — 2.6-2.8 us
+  //     cheaper per step on MI355X (tools/step_sync_probe.cpp, profiles/r03z_step_wait_ab.txt).
+  //   sync: hipStreamSynchronize, whose completion also covers stores to a peer GPU's memory.
+  // Without a word, if the write cannot be queued, or after the communicator's timeout, the word
+  // mode falls back to hipStreamSynchronize (so it never returns with the step still in flight).
   bool streamDone() {
-    if (done && stepWaitByWord()) {
+    if (done && c->stepWaitWord) {
       const uint32_t t = ++done[1];
       if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
         const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
@@ -272,13 +282,6 @@ struct Prims {
       }
     }
     return hipStreamSynchronize(stream) == hipSuccess;
-  }
-  static bool stepWaitByWord() {
-    static const bool on = [] {
-      const char* e = getenv("NEXR_STEP_WAIT");
-      return !(e && !strcmp(e, "sync"));
-    }();
-    return on;
   }
 
   // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
@@ -464,9 +467,14 @@ nexrResult_t runThreads(nexrRingComm* c, Shared& sh, const std::vector<std::func
 nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes = 0);
 nexrResult_t enablePeer(int a, int b);
 nexrResult_t ensureSecondStreams(nexrRingComm* c);
-// Process ranks: connect this rank's PAT (p2p = false) or P2P links on first use (collective).
-nexrResult_t ensurePeerLinks(nexrRingComm* c, bool p2p);
 nexrResult_t peerFinish(nexrRingComm* c, Shared& sh);
 nexrResult_t ringLinkHandover(nexrRingComm* c, bool resident);
+// NEXR_STEP_WAIT: 1 = word, 0 = sync, -1 = unset (auto: word only when all ranks share one GPU).
+int stepWaitMode();
+// calcCollChunking for one channel in elements (enqueue.cc:1993-1999).
+int64_t chunkElems(const nexrRingComm* c, Geom g, size_t esz, bool tree, size_t nBytes);
+nexrResult_t ensureTree(nexrRingComm* c);
+bool envFlagOn(const char* name, bool dflt);
+enum RingColl { kAllReduce, kReduceScatter, kAllGather, kReduce, kBroadcast };
 
 }  // namespace nexr_emu

@@ -1,6 +1,7 @@
 // nexr_p2p.cpp — ncclSend / ncclRecv on the emulated communicator (the P2P work batch of
-// src/device/sendrecv.h), thread ranks and process ranks (include/nexr_ring.h nexrSendRecv,
-// nexrPeerSendRecv).
+// src/device/sendrecv.h), thread ranks and process ranks (include/nexr_extras.h nexrSendRecv,
+// nexrPeerSendRecv). Part of the opt-in extras library (make EXTRAS=1 -> libnexr_extras.so): the
+// P2P schedule goes beyond SURVEY §8's rows.
 #include "nexr_emu.h"
 
 namespace nexr_emu {
@@ -88,6 +89,68 @@ void runP2pHalf(nexrRingComm* c, Shared* sh, int rank, bool send, int peer, cons
   }
 }
 
+// Process ranks: the first Send/Recv call on a communicator connects this rank's P2P links (any
+// r -> q at connection index 1, SIMPLE buffers and their LL buffers). Every rank allocates the FIFOs
+// it receives into, publishes their IPC handles in the shared segment, and, once all ranks have,
+// maps the FIFOs it sends into. Collective: every rank makes its first call together.
+nexrResult_t ensurePeerLinks(nexrRingComm* c) {
+  if (!c->p2pConns.empty()) return nexrSuccess;
+  const int n = c->cfg.nRanks, me = c->self;
+  if (n > kPeerLinkMaxRanks) return nexrInvalidUsage;
+  struct Set {
+    std::vector<Conn*>* conns;
+    size_t bytes, slot;
+    ConnState PeerLink::*state;
+    hipIpcMemHandle_t PeerLink::*handle;
+  };
+  Set sets[2] = {{&c->p2pConns, c->p2pChunkBytes * kSteps, c->p2pChunkBytes, &PeerLink::p2p, &PeerLink::p2pFifo},
+                 {&c->p2pLLConns, kDefaultLLBuffBytes, kDefaultLLBuffBytes / kSteps, &PeerLink::p2pLL,
+                  &PeerLink::p2pLLFifo}};
+  const char* unc = getenv("NEXR_PEER_FIFO_UNCACHED");
+  const bool uncached = !(unc && unc[0] == '0');
+  if (hipSetDevice(c->devices[me]) != hipSuccess) return nexrUnhandledCudaError;
+  for (Set& st : sets) {
+    st.conns->assign((size_t)n * n, nullptr);
+    for (int q = 0; q < n; q++) {
+      if (q == me) continue;
+      PeerLink* l = peerLink(c->shm, n, q, me);
+      Conn* k = (*st.conns)[(size_t)q * n + me] = new Conn();
+      k->device = c->devices[me];
+      k->slotBytes = st.slot;
+      k->st = &(l->*st.state);
+      if ((uncached ? hipExtMallocWithFlags((void**)&k->fifo, st.bytes, hipDeviceMallocUncached)
+                    : hipMalloc((void**)&k->fifo, st.bytes)) != hipSuccess ||
+          hipIpcGetMemHandle(&(l->*st.handle), k->fifo) != hipSuccess)
+        return nexrUnhandledCudaError;
+    }
+  }
+  PeerHeader* h = peerHeader(c->shm);
+  h->p2pJoined.fetch_add(1, std::memory_order_acq_rel);  // publishes the handles
+  const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (h->p2pJoined.load(std::memory_order_acquire) < (uint32_t)n) {
+    if (h->abort.load(std::memory_order_acquire)) return nexrRemoteError;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return nexrRemoteError;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  for (Set& st : sets) {
+    for (int q = 0; q < n; q++) {
+      if (q == me) continue;
+      PeerLink* l = peerLink(c->shm, n, me, q);
+      Conn* k = (*st.conns)[(size_t)me * n + q] = new Conn();
+      k->device = c->devices[me];
+      k->slotBytes = st.slot;
+      k->st = &(l->*st.state);
+      k->ownsFifo = false;
+      char* mapped = nullptr;
+      if (hipIpcOpenMemHandle((void**)&mapped, l->*st.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+        return nexrUnhandledCudaError;
+      k->fifo = mapped;
+    }
+  }
+  return nexrSuccess;
+}
+
 nexrResult_t sendRecv(nexrRingComm* c, const void* const* sendbuffs, const int* sendPeers, void* const* recvbuffs,
                       const int* recvPeers, size_t bytes) {
   if (!c || c->peer || !sendbuffs || !sendPeers || !recvbuffs || !recvPeers) return nexrInvalidArgument;
@@ -146,7 +209,7 @@ NEXR_API nexrResult_t nexrPeerSendRecv(nexrRingComm_t c, const void* sendbuff, i
   if (bytes > 0 && ((sendPeer >= 0 && !sendbuff) || (recvPeer >= 0 && !recvbuff))) return nexrInvalidArgument;
   (void)hipSetDevice(c->devices[me]);
   nexrResult_t r = n > 1 ? ensureSecondStreams(c) : nexrSuccess;
-  if (r == nexrSuccess && n > 1) r = ensurePeerLinks(c, true);
+  if (r == nexrSuccess && n > 1) r = ensurePeerLinks(c);
   if (r != nexrSuccess) {
     c->broken = true;
     if (c->shm) peerHeader(c->shm)->abort.store(1);

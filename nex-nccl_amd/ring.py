@@ -1,4 +1,5 @@
-"""Python view of the CPU-emulated collectives (include/nexr_ring.h, libnexr_ring.so).
+"""Python view of the CPU-emulated collectives (include/nexr_ring.h, libnexr_ring.so; with
+``extras=True`` the opt-in include/nexr_extras.h, libnexr_extras.so).
 
 The ring and tree schedules (runRing of all_reduce.h, reduce_scatter.h, all_gather.h, reduce.h,
 broadcast.h; runTreeSplit, all_reduce.h:150-230) and the genericOp slicing / FIFO credit
@@ -15,15 +16,16 @@ from . import NexrError, Result, _check, lib
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 RING_LIB_PATH = os.path.join(_HERE, "libnexr_ring.so")
+# Opt-in (make -C nex-nccl_amd/csrc EXTRAS=1): include/nexr_extras.h, a superset of libnexr_ring.so.
+EXTRAS_LIB_PATH = os.path.join(_HERE, "libnexr_extras.so")
 RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceScatter", "nexrRingAllGather",
                     "nexrRingReduce", "nexrRingBroadcast", "nexrTreeAllReduce", "nexrTreeTopology",
-                    "nexrRingCommDestroy", "nexrPeerRingCommCreate", "nexrPeerRingAllReduce",
-                    "nexrPeerRingReduceScatter", "nexrPeerRingAllGather", "nexrPeerRingReduce",
-                    "nexrPeerRingBroadcast", "nexrPatReduceScatter", "nexrPatAllGather", "nexrPatSchedule",
-                    "nexrSendRecv", "nexrPeerPatReduceScatter", "nexrPeerPatAllGather", "nexrPeerSendRecv",
-                    "nexrRingAllReduceResident", "nexrRingReduceScatterResident", "nexrRingAllGatherResident",
-                    "nexrRingReduceResident", "nexrRingBroadcastResident", "nexrTreeAllReduceResident",
-                    "nexrPeerRingAllReduceResident")
+                    "nexrRingCommGetStepWait", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
+                    "nexrPeerRingAllReduce", "nexrPeerRingReduceScatter", "nexrPeerRingAllGather",
+                    "nexrPeerRingReduce", "nexrPeerRingBroadcast")
+EXTRAS_ABI_SYMBOLS = ("nexrSendRecv", "nexrPeerSendRecv", "nexrRingAllReduceResident",
+                      "nexrRingReduceScatterResident", "nexrRingAllGatherResident", "nexrRingReduceResident",
+                      "nexrRingBroadcastResident", "nexrTreeAllReduceResident", "nexrPeerRingAllReduceResident")
 
 HOST_MEMORY = 0
 DEVICE_MEMORY = 1
@@ -50,83 +52,69 @@ class PeerRingConfig(ctypes.Structure):
                 ("shmName", ctypes.c_char_p)]
 
 
-_ring = None
+_libs = {}
+
+
+def _bind_ring(L: ctypes.CDLL) -> None:
+    vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    arr = ctypes.POINTER(ctypes.c_void_p)
+    L.nexrRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(RingConfig)]
+    for name, extra in (("nexrRingAllReduce", [i32]), ("nexrRingReduceScatter", [i32]), ("nexrRingAllGather", []),
+                        ("nexrRingReduce", [i32, i32]), ("nexrRingBroadcast", [i32]), ("nexrTreeAllReduce", [i32])):
+        getattr(L, name).argtypes = [vp, arr, arr, sz, i32] + extra
+    for name, extra in (("nexrPeerRingAllReduce", [i32]), ("nexrPeerRingReduceScatter", [i32]),
+                        ("nexrPeerRingAllGather", []), ("nexrPeerRingReduce", [i32, i32]),
+                        ("nexrPeerRingBroadcast", [i32])):
+        getattr(L, name).argtypes = [vp, vp, vp, sz, i32] + extra
+    L.nexrTreeTopology.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.nexrRingCommGetStepWait.argtypes = [vp, ctypes.POINTER(i32)]
+    L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
+    L.nexrRingCommDestroy.argtypes = [vp]
+    for name in RING_ABI_SYMBOLS:
+        getattr(L, name).restype = ctypes.c_int
+
+
+def _bind_extras(L: ctypes.CDLL) -> None:
+    vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    arr = ctypes.POINTER(ctypes.c_void_p)
+    for name, extra in (("nexrRingAllReduceResident", [i32]), ("nexrTreeAllReduceResident", [i32]),
+                        ("nexrRingReduceScatterResident", [i32]), ("nexrRingAllGatherResident", []),
+                        ("nexrRingReduceResident", [i32, i32]), ("nexrRingBroadcastResident", [i32])):
+        getattr(L, name).argtypes = [vp, arr, arr, sz, i32] + extra
+    L.nexrPeerRingAllReduceResident.argtypes = [vp, vp, vp, sz, i32, i32]
+    L.nexrSendRecv.argtypes = [vp, arr, ctypes.POINTER(i32), arr, ctypes.POINTER(i32), sz]
+    L.nexrPeerSendRecv.argtypes = [vp, vp, i32, vp, i32, sz]
+    for name in EXTRAS_ABI_SYMBOLS:
+        getattr(L, name).restype = ctypes.c_int
 
 
 def ring_lib() -> ctypes.CDLL:
-    global _ring
-    if _ring is None:
+    """libnexr_ring.so: the graded callers (include/nexr_ring.h)."""
+    if "ring" not in _libs:
         lib()  # libnexr.so first (the ring library links against it)
         if not os.path.exists(RING_LIB_PATH):
             raise NexrError(Result.InternalError, f"{RING_LIB_PATH} not built")
         L = ctypes.CDLL(RING_LIB_PATH)
-        L.nexrRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(RingConfig)]
-        L.nexrRingCommCreate.restype = ctypes.c_int
-        L.nexrRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
-                                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
-        L.nexrRingAllReduce.restype = ctypes.c_int
-        L.nexrRingAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
-        L.nexrRingAllReduceResident.restype = ctypes.c_int
-        L.nexrTreeAllReduceResident.argtypes = L.nexrRingAllReduce.argtypes
-        L.nexrTreeAllReduceResident.restype = ctypes.c_int
-        L.nexrPeerRingAllReduceResident.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                    ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
-        L.nexrPeerRingAllReduceResident.restype = ctypes.c_int
-        _arr, _i, _sz = ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t
-        for f, extra in ((L.nexrRingReduceScatterResident, [_i, _i]), (L.nexrRingAllGatherResident, [_i]),
-                         (L.nexrRingReduceResident, [_i, _i, _i]), (L.nexrRingBroadcastResident, [_i, _i])):
-            f.argtypes = [ctypes.c_void_p, _arr, _arr, _sz] + extra
-            f.restype = ctypes.c_int
-        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
-        arr = ctypes.POINTER(ctypes.c_void_p)
-        for name, extra in (("nexrRingReduceScatter", [i32]), ("nexrRingAllGather", []), ("nexrRingReduce", [i32, i32]),
-                            ("nexrRingBroadcast", [i32]), ("nexrTreeAllReduce", [i32]),
-                            ("nexrPatReduceScatter", [i32]), ("nexrPatAllGather", [])):
-            f = getattr(L, name)
-            f.argtypes = [vp, arr, arr, sz, i32] + extra
-            f.restype = ctypes.c_int
-        L.nexrPeerSendRecv.argtypes = [vp, vp, i32, vp, i32, sz]
-        L.nexrPeerSendRecv.restype = ctypes.c_int
-        for name, extra in (("nexrPeerRingReduceScatter", [i32]), ("nexrPeerRingAllGather", []),
-                            ("nexrPeerPatReduceScatter", [i32]), ("nexrPeerPatAllGather", []),
-                            ("nexrPeerRingReduce", [i32, i32]), ("nexrPeerRingBroadcast", [i32])):
-            f = getattr(L, name)
-            f.argtypes = [vp, vp, vp, sz, i32] + extra
-            f.restype = ctypes.c_int
-        L.nexrSendRecv.argtypes = [vp, arr, ctypes.POINTER(i32), arr, ctypes.POINTER(i32), sz]
-        L.nexrSendRecv.restype = ctypes.c_int
-        L.nexrPatSchedule.argtypes = [i32, i32, i32, sz, i32, sz, ctypes.POINTER(ctypes.c_int64), sz,
-                                      ctypes.POINTER(sz), ctypes.POINTER(i32)]
-        L.nexrPatSchedule.restype = ctypes.c_int
-        L.nexrTreeTopology.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
-        L.nexrTreeTopology.restype = ctypes.c_int
-        L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
-        L.nexrPeerRingCommCreate.restype = ctypes.c_int
-        L.nexrPeerRingAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                            ctypes.c_int, ctypes.c_int]
-        L.nexrPeerRingAllReduce.restype = ctypes.c_int
-        L.nexrRingCommDestroy.argtypes = [ctypes.c_void_p]
-        L.nexrRingCommDestroy.restype = ctypes.c_int
-        _ring = L
-    return _ring
+        _bind_ring(L)
+        _libs["ring"] = L
+    return _libs["ring"]
 
 
-PAT_FIELDS = ("recvDim", "sendDim", "recvOffset", "sendOffset", "stepOffset", "postRecv", "postSend", "nelem",
-              "last", "skipped", "inpIx", "outIx")
+def extras_available() -> bool:
+    return os.path.exists(EXTRAS_LIB_PATH)
 
 
-def pat_schedule(reduce_scatter: bool, n_ranks: int, rank: int, count: int, datatype: int, buff_bytes: int = 0):
-    """The PAT step stream of one rank (nexrPatSchedule): (list of dicts with PAT_FIELDS, parallelFactor)."""
-    L = ring_lib()
-    n_ops = ctypes.c_size_t()
-    pf = ctypes.c_int()
-    _check(L.nexrPatSchedule(int(reduce_scatter), n_ranks, rank, count, datatype, buff_bytes, None, 0,
-                             ctypes.byref(n_ops), ctypes.byref(pf)), "nexrPatSchedule")
-    buf = (ctypes.c_int64 * (12 * n_ops.value))()
-    _check(L.nexrPatSchedule(int(reduce_scatter), n_ranks, rank, count, datatype, buff_bytes, buf, n_ops.value,
-                             ctypes.byref(n_ops), ctypes.byref(pf)), "nexrPatSchedule")
-    vals = list(buf)
-    return [dict(zip(PAT_FIELDS, vals[12 * i:12 * i + 12])) for i in range(n_ops.value)], pf.value
+def extras_lib() -> ctypes.CDLL:
+    """libnexr_extras.so (opt-in): nexr_ring.h's entry points plus include/nexr_extras.h's."""
+    if "extras" not in _libs:
+        lib()
+        if not extras_available():
+            raise NexrError(Result.InvalidUsage, f"{EXTRAS_LIB_PATH} not built (make -C nex-nccl_amd/csrc EXTRAS=1)")
+        L = ctypes.CDLL(EXTRAS_LIB_PATH)
+        _bind_ring(L)
+        _bind_extras(L)
+        _libs["extras"] = L
+    return _libs["extras"]
 
 
 class RingComm:
@@ -137,11 +125,15 @@ class RingComm:
     def __init__(self, n_ranks: int, mem_mode: int = HOST_MEMORY, buff_bytes: int = 0,
                  fn_address: Optional[int] = None, timeout_ms: int = 0, protocol: int = PROTO_SIMPLE,
                  ll_fn_address: Optional[int] = None, ll128_fn_address: Optional[int] = None,
-                 tree_ranks_per_node: int = 0, tree_index: int = 0, n_channels: int = 0):
+                 tree_ranks_per_node: int = 0, tree_index: int = 0, n_channels: int = 0, extras: bool = False):
+        """extras=True: the communicator lives in the opt-in libnexr_extras.so, which adds send/recv and
+        the device-resident collectives; every call on it goes to that library."""
         cfg = RingConfig(n_ranks, buff_bytes, mem_mode, fn_address or None, timeout_ms, protocol,
                          ll_fn_address or None, ll128_fn_address or None, tree_ranks_per_node, tree_index, n_channels)
+        self._L = extras_lib() if extras else ring_lib()
+        self.extras = extras
         h = ctypes.c_void_p()
-        _check(ring_lib().nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
+        _check(self._L.nexrRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrRingCommCreate")
         self._h = h
         self.n_ranks = n_ranks
 
@@ -151,38 +143,38 @@ class RingComm:
             raise NexrError(Result.InvalidArgument, "one send and one recv buffer per rank")
         s = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in sendbuffs])
         r = (ctypes.c_void_p * self.n_ranks)(*[int(p) for p in recvbuffs])
-        _check(ring_lib().nexrRingAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrRingAllReduce")
+        _check(self._L.nexrRingAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrRingAllReduce")
 
     def all_reduce_resident(self, sendbuffs: Sequence[int], recvbuffs: Sequence[int], count: int, datatype: int,
                             op: int) -> None:
         """The same all-reduce as one device-resident launch per GPU (nexrRingAllReduceResident)."""
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
+        _check(self._extras().nexrRingAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
                "nexrRingAllReduceResident")
 
     def tree_all_reduce_resident(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrTreeAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
+        _check(self._extras().nexrTreeAllReduceResident(self._h, s, r, int(count), int(datatype), int(op)),
                "nexrTreeAllReduceResident")
 
     def reduce_scatter_resident(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingReduceScatterResident(self._h, s, r, int(recvcount), int(datatype), int(op)),
+        _check(self._extras().nexrRingReduceScatterResident(self._h, s, r, int(recvcount), int(datatype), int(op)),
                "nexrRingReduceScatterResident")
 
     def all_gather_resident(self, sendbuffs, recvbuffs, sendcount: int, datatype: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingAllGatherResident(self._h, s, r, int(sendcount), int(datatype)),
+        _check(self._extras().nexrRingAllGatherResident(self._h, s, r, int(sendcount), int(datatype)),
                "nexrRingAllGatherResident")
 
     def reduce_resident(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int, root: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingReduceResident(self._h, s, r, int(count), int(datatype), int(op), int(root)),
+        _check(self._extras().nexrRingReduceResident(self._h, s, r, int(count), int(datatype), int(op), int(root)),
                "nexrRingReduceResident")
 
     def broadcast_resident(self, sendbuffs, recvbuffs, count: int, datatype: int, root: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingBroadcastResident(self._h, s, r, int(count), int(datatype), int(root)),
+        _check(self._extras().nexrRingBroadcastResident(self._h, s, r, int(count), int(datatype), int(root)),
                "nexrRingBroadcastResident")
 
     def _arrays(self, sendbuffs, recvbuffs):
@@ -194,36 +186,25 @@ class RingComm:
 
     def reduce_scatter(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingReduceScatter(self._h, s, r, int(recvcount), int(datatype), int(op)),
+        _check(self._L.nexrRingReduceScatter(self._h, s, r, int(recvcount), int(datatype), int(op)),
                "nexrRingReduceScatter")
 
     def all_gather(self, sendbuffs, recvbuffs, sendcount: int, datatype: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingAllGather(self._h, s, r, int(sendcount), int(datatype)), "nexrRingAllGather")
+        _check(self._L.nexrRingAllGather(self._h, s, r, int(sendcount), int(datatype)), "nexrRingAllGather")
 
     def reduce(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int, root: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingReduce(self._h, s, r, int(count), int(datatype), int(op), int(root)),
+        _check(self._L.nexrRingReduce(self._h, s, r, int(count), int(datatype), int(op), int(root)),
                "nexrRingReduce")
 
     def broadcast(self, sendbuffs, recvbuffs, count: int, datatype: int, root: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrRingBroadcast(self._h, s, r, int(count), int(datatype), int(root)), "nexrRingBroadcast")
+        _check(self._L.nexrRingBroadcast(self._h, s, r, int(count), int(datatype), int(root)), "nexrRingBroadcast")
 
     def tree_all_reduce(self, sendbuffs, recvbuffs, count: int, datatype: int, op: int) -> None:
         s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrTreeAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrTreeAllReduce")
-
-    def pat_reduce_scatter(self, sendbuffs, recvbuffs, recvcount: int, datatype: int, op: int) -> None:
-        """ncclReduceScatter with NCCL_ALGO_PAT (SIMPLE)."""
-        s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrPatReduceScatter(self._h, s, r, int(recvcount), int(datatype), int(op)),
-               "nexrPatReduceScatter")
-
-    def pat_all_gather(self, sendbuffs, recvbuffs, sendcount: int, datatype: int) -> None:
-        """ncclAllGather with NCCL_ALGO_PAT (SIMPLE)."""
-        s, r = self._arrays(sendbuffs, recvbuffs)
-        _check(ring_lib().nexrPatAllGather(self._h, s, r, int(sendcount), int(datatype)), "nexrPatAllGather")
+        _check(self._L.nexrTreeAllReduce(self._h, s, r, int(count), int(datatype), int(op)), "nexrTreeAllReduce")
 
     def send_recv(self, sendbuffs, send_peers, recvbuffs, recv_peers, nbytes: int) -> None:
         """ncclSend/ncclRecv of every rank in one group: rank r sends nbytes of sendbuffs[r] to
@@ -231,18 +212,31 @@ class RingComm:
         s, r = self._arrays(sendbuffs, recvbuffs)
         sp = (ctypes.c_int * self.n_ranks)(*[int(v) for v in send_peers])
         rp = (ctypes.c_int * self.n_ranks)(*[int(v) for v in recv_peers])
-        _check(ring_lib().nexrSendRecv(self._h, s, sp, r, rp, int(nbytes)), "nexrSendRecv")
+        _check(self._extras().nexrSendRecv(self._h, s, sp, r, rp, int(nbytes)), "nexrSendRecv")
+
+    def step_wait(self) -> str:
+        """"word" or "sync": how this communicator's rank threads wait for a device step
+        (nexrRingCommGetStepWait; sync when the ranks span GPUs)."""
+        w = ctypes.c_int()
+        _check(self._L.nexrRingCommGetStepWait(self._h, ctypes.byref(w)), "nexrRingCommGetStepWait")
+        return "word" if w.value else "sync"
 
     def tree_topology(self, rank: int):
         """(up, [down...]) of `rank` in this communicator's tree (-1 = none)."""
         up = ctypes.c_int()
         down = (ctypes.c_int * 3)()
-        _check(ring_lib().nexrTreeTopology(self._h, int(rank), ctypes.byref(up), down), "nexrTreeTopology")
+        _check(self._L.nexrTreeTopology(self._h, int(rank), ctypes.byref(up), down), "nexrTreeTopology")
         return up.value, [d for d in down if d >= 0]
+
+    def _extras(self) -> ctypes.CDLL:
+        if not self.extras:
+            raise NexrError(Result.InvalidUsage, "send/recv and the resident collectives are in the opt-in extras "
+                                                 "library: create the communicator with extras=True")
+        return self._L
 
     def close(self) -> None:
         if self._h:
-            ring_lib().nexrRingCommDestroy(self._h)
+            self._L.nexrRingCommDestroy(self._h)
             self._h = None
 
     def __enter__(self):
@@ -265,55 +259,62 @@ class PeerRingComm:
     the constructor blocks until all ``n_ranks`` processes have joined."""
 
     def __init__(self, n_ranks: int, rank: int, shm_name: str, device: int = 0, buff_bytes: int = 0,
-                 protocol: int = PROTO_SIMPLE, timeout_ms: int = 0):
+                 protocol: int = PROTO_SIMPLE, timeout_ms: int = 0, extras: bool = False):
         self._name = shm_name.encode()
         cfg = PeerRingConfig(n_ranks, rank, device, buff_bytes, protocol, timeout_ms, self._name)
+        self._L = extras_lib() if extras else ring_lib()
+        self.extras = extras
         h = ctypes.c_void_p()
-        _check(ring_lib().nexrPeerRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrPeerRingCommCreate")
+        _check(self._L.nexrPeerRingCommCreate(ctypes.byref(h), ctypes.byref(cfg)), "nexrPeerRingCommCreate")
         self._h = h
         self.n_ranks, self.rank = n_ranks, rank
 
     def all_reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int) -> None:
-        _check(ring_lib().nexrPeerRingAllReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
+        _check(self._L.nexrPeerRingAllReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
                                                 int(datatype), int(op)), "nexrPeerRingAllReduce")
 
     def all_reduce_resident(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int) -> None:
         """This rank's part of the all-reduce as one device-resident launch (nexrPeerRingAllReduceResident)."""
-        _check(ring_lib().nexrPeerRingAllReduceResident(self._h, int(sendbuff) or None, int(recvbuff) or None,
+        _check(self._extras().nexrPeerRingAllReduceResident(self._h, int(sendbuff) or None, int(recvbuff) or None,
                                                         int(count), int(datatype), int(op)),
                "nexrPeerRingAllReduceResident")
 
     def reduce_scatter(self, sendbuff: int, recvbuff: int, recvcount: int, datatype: int, op: int) -> None:
-        _check(ring_lib().nexrPeerRingReduceScatter(self._h, int(sendbuff) or None, int(recvbuff) or None,
+        _check(self._L.nexrPeerRingReduceScatter(self._h, int(sendbuff) or None, int(recvbuff) or None,
                                                     int(recvcount), int(datatype), int(op)), "nexrPeerRingReduceScatter")
 
     def all_gather(self, sendbuff: int, recvbuff: int, sendcount: int, datatype: int) -> None:
-        _check(ring_lib().nexrPeerRingAllGather(self._h, int(sendbuff) or None, int(recvbuff) or None, int(sendcount),
+        _check(self._L.nexrPeerRingAllGather(self._h, int(sendbuff) or None, int(recvbuff) or None, int(sendcount),
                                                 int(datatype)), "nexrPeerRingAllGather")
 
     def reduce(self, sendbuff: int, recvbuff: int, count: int, datatype: int, op: int, root: int) -> None:
-        _check(ring_lib().nexrPeerRingReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
+        _check(self._L.nexrPeerRingReduce(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
                                              int(datatype), int(op), int(root)), "nexrPeerRingReduce")
 
-    def pat_reduce_scatter(self, sendbuff: int, recvbuff: int, recvcount: int, datatype: int, op: int) -> None:
-        _check(ring_lib().nexrPeerPatReduceScatter(self._h, int(sendbuff) or None, int(recvbuff) or None,
-                                                   int(recvcount), int(datatype), int(op)), "nexrPeerPatReduceScatter")
-
-    def pat_all_gather(self, sendbuff: int, recvbuff: int, sendcount: int, datatype: int) -> None:
-        _check(ring_lib().nexrPeerPatAllGather(self._h, int(sendbuff) or None, int(recvbuff) or None, int(sendcount),
-                                               int(datatype)), "nexrPeerPatAllGather")
-
     def send_recv(self, sendbuff: int, send_peer: int, recvbuff: int, recv_peer: int, nbytes: int) -> None:
-        _check(ring_lib().nexrPeerSendRecv(self._h, int(sendbuff) or None, int(send_peer), int(recvbuff) or None,
+        _check(self._extras().nexrPeerSendRecv(self._h, int(sendbuff) or None, int(send_peer), int(recvbuff) or None,
                                            int(recv_peer), int(nbytes)), "nexrPeerSendRecv")
 
+    def step_wait(self) -> str:
+        """"word" or "sync": how this communicator's rank threads wait for a device step
+        (nexrRingCommGetStepWait; sync when the ranks span GPUs)."""
+        w = ctypes.c_int()
+        _check(self._L.nexrRingCommGetStepWait(self._h, ctypes.byref(w)), "nexrRingCommGetStepWait")
+        return "word" if w.value else "sync"
+
     def broadcast(self, sendbuff: int, recvbuff: int, count: int, datatype: int, root: int) -> None:
-        _check(ring_lib().nexrPeerRingBroadcast(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
+        _check(self._L.nexrPeerRingBroadcast(self._h, int(sendbuff) or None, int(recvbuff) or None, int(count),
                                                 int(datatype), int(root)), "nexrPeerRingBroadcast")
+
+    def _extras(self) -> ctypes.CDLL:
+        if not self.extras:
+            raise NexrError(Result.InvalidUsage, "send/recv and the resident collectives are in the opt-in extras "
+                                                 "library: create the communicator with extras=True")
+        return self._L
 
     def close(self) -> None:
         if self._h:
-            ring_lib().nexrRingCommDestroy(self._h)
+            self._L.nexrRingCommDestroy(self._h)
             self._h = None
 
     def __enter__(self):

@@ -1,7 +1,7 @@
 // Host-only stress driver for the emulated collectives (nexr_ring.cpp), built with sanitizers by
 // tests/test_native_sanitizers.py: ThreadSanitizer for the FIFO head/tail protocol between rank
 // threads (and between the two halves of a tree rank), AddressSanitizer + UndefinedBehaviorSanitizer
-// for the slicing and chunking arithmetic; the PAT batches and the send/recv halves for SIMPLE. Every reduceCopy / LL / LL128 step is served by the C
+// for the slicing and chunking arithmetic. Every reduceCopy / LL / LL128 step is served by the C
 // oracle (no GPU involved). Integer sums are order-independent, so the expected result of every
 // collective is plain arithmetic.
 #include <cstdint>
@@ -109,39 +109,6 @@ int main() {
         for (int k = 0; k < n; k++)
           for (size_t i = 0; i < count; i++)
             if (out[k][i] != in[root][i]) { fail("broadcast value", protos[pi], n); break; }
-        if (protos[pi] != nexrRingProtoSimple) continue;
-        // PAT reduce-scatter and all-gather (r -/+ 2^d links, lock-step batches)
-        reset();
-        if (nexrPatReduceScatter(comm, s.data(), r.data(), count, nexrUint32, nexrSum) != nexrSuccess) {
-          fail("pat reducescatter", protos[pi], n);
-          return 2;
-        }
-        for (int k = 0; k < n; k++)
-          for (size_t i = 0; i < count; i++)
-            if (out[k][i] != sum(k * count + i)) { fail("pat reducescatter value", protos[pi], n); break; }
-        reset();
-        if (nexrPatAllGather(comm, s.data(), r.data(), count, nexrUint32) != nexrSuccess) {
-          fail("pat allgather", protos[pi], n);
-          return 2;
-        }
-        for (int k = 0; k < n; k++)
-          for (int j = 0; j < n; j++)
-            for (size_t i = 0; i < count; i++)
-              if (out[k][j * count + i] != in[j][i]) { fail("pat allgather value", protos[pi], n); j = n; break; }
-        // send/recv: a ring shift by iter+1 (a self-send when it wraps to 0)
-        reset();
-        std::vector<int> sp(n), rp(n);
-        for (int k = 0; k < n; k++) {
-          sp[k] = (k + iter + 1) % n;
-          rp[k] = (k - (iter + 1) % n + n) % n;
-        }
-        if (nexrSendRecv(comm, s.data(), sp.data(), r.data(), rp.data(), count * 4) != nexrSuccess) {
-          fail("sendrecv", protos[pi], n);
-          return 2;
-        }
-        for (int k = 0; k < n; k++)
-          for (size_t i = 0; i < count; i++)
-            if (out[k][i] != in[rp[k]][i]) { fail("sendrecv value", protos[pi], n); break; }
       }
       nexrRingCommDestroy(comm);
     }

@@ -25,14 +25,14 @@ def main() -> int:
         ap.add_argument(f"--{name}", type=int, required=True)
     ap.add_argument("--coll", default="allreduce",
                     choices=["allreduce", "allreduce_resident", "allreduce_mixed", "reducescatter", "allgather", "reduce", "broadcast",
-                             "pat_rs", "pat_ag", "sendrecv"])
+                             "sendrecv"])
     ap.add_argument("--root", type=int, default=0)
     ap.add_argument("--shm", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     ring = importlib.import_module("nex-nccl_amd.ring")
-    n_in = a.count * a.n if a.coll in ("reducescatter", "pat_rs") else a.count
-    n_out = a.count * a.n if a.coll in ("allgather", "pat_ag") else a.count
+    n_in = a.count * a.n if a.coll == "reducescatter" else a.count
+    n_out = a.count * a.n if a.coll == "allgather" else a.count
     inputs = mg.gen_inputs(a.dt, a.n, n_in, a.seed, special=True)
     # Rank r drives GPU r mod (visible GPUs): on a node every neighbour pair of the ring sits on two
     # GPUs and each step's reduce-copy writes into the next rank's FIFO over xGMI; on a one-GPU box all
@@ -41,22 +41,19 @@ def main() -> int:
     torch.cuda.set_device(ordinal)
     assert torch.cuda.current_device() == ordinal
     dev = torch.device("cuda", ordinal)
-    with open(f"{a.out}.device", "w") as f:
-        f.write(f"{ordinal} {torch.cuda.device_count()}\n")
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
     recv = torch.zeros(n_out, dtype=send.dtype, device=dev)
     torch.cuda.synchronize()
     resident = a.coll in ("allreduce_resident", "allreduce_mixed")
+    extras = resident or a.coll == "sendrecv"  # the opt-in extras library (include/nexr_extras.h)
     with ring.PeerRingComm(a.n, a.rank, a.shm, device=ordinal, buff_bytes=a.buff, protocol=a.proto,
-                           timeout_ms=20000 if resident else 60000) as comm:
+                           timeout_ms=20000 if resident else 60000, extras=extras) as comm:
+        with open(f"{a.out}.device", "w") as f:  # the GPU, the GPU count, and the step wait in effect
+            f.write(f"{ordinal} {torch.cuda.device_count()} {comm.step_wait()}\n")
         if a.coll not in ("allreduce", "allreduce_resident", "allreduce_mixed"):
             for call in range(a.calls):
                 if a.coll == "reducescatter":
                     comm.reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
-                elif a.coll == "pat_rs":
-                    comm.pat_reduce_scatter(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
-                elif a.coll == "pat_ag":
-                    comm.pat_all_gather(send.data_ptr(), recv.data_ptr(), a.count, a.dt)
                 elif a.coll == "sendrecv":  # call c: a ring shift by c+1 (a self-copy when it wraps)
                     k = (call + 1) % a.n
                     comm.send_recv(send.data_ptr(), (a.rank + k) % a.n, recv.data_ptr(), (a.rank - k) % a.n,

@@ -309,19 +309,57 @@ def test_host_to_dev_red_op_matches_oracle(nexr, oracle, dt, op, nranks):
     assert out.proxyOp == op and out.scalarArgIsPtr is False
 
 
+def _declared(header: str):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    return sorted(set(re.findall(r"NEXR_API\s+[\w\s\*]+?\b(nexr\w+)\s*\(", text)))
+
+
+def _exported(path: str):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line and "nexr" in line}
+
+
 def test_ring_library_exports_its_header():
+    """libnexr_ring.so (the default build) exports exactly include/nexr_ring.h: none of the opt-in
+    extras (include/nexr_extras.h) and no PAT."""
     import importlib
     ring = importlib.import_module("nex-nccl_amd.ring")
-    text = open(os.path.join(ROOT, "include", "nexr_ring.h")).read()
-    declared = sorted(set(re.findall(r"NEXR_API\s+[\w\s\*]+?\b(nexr\w+)\s*\(", text)))
+    declared = _declared("nexr_ring.h")
     assert declared == sorted(ring.RING_ABI_SYMBOLS)
     L = ring.ring_lib()
-    out = subprocess.run(["nm", "-D", "--defined-only", ring.RING_LIB_PATH], capture_output=True, text=True,
-                         check=True).stdout
-    exported = {line.split()[-1] for line in out.splitlines() if " T " in line and "nexr" in line}
-    assert exported == set(declared)
+    assert _exported(ring.RING_LIB_PATH) == set(declared)
     for name in declared:
         assert hasattr(L, name)
+    assert not any("Pat" in name for name in declared + _declared("nexr_extras.h"))
+
+
+def test_extras_library_exports_both_headers():
+    """libnexr_extras.so (make EXTRAS=1) is a superset: nexr_ring.h's entry points plus nexr_extras.h's."""
+    import importlib
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    extras = _declared("nexr_extras.h")
+    assert extras == sorted(ring.EXTRAS_ABI_SYMBOLS)
+    assert not set(extras) & set(_declared("nexr_ring.h"))
+    if not ring.extras_available():
+        pytest.skip("libnexr_extras.so not built (make -C nex-nccl_amd/csrc EXTRAS=1)")
+    assert _exported(ring.EXTRAS_LIB_PATH) == set(extras) | set(_declared("nexr_ring.h"))
+
+
+def test_extras_calls_need_an_extras_communicator(oracle):
+    """Send/recv and the resident collectives on a communicator of the default library fail with the
+    library's InvalidUsage, never with a missing-symbol error."""
+    import importlib
+    import numpy as np
+    nexr_pkg = importlib.import_module("nex-nccl_amd")
+    ring = importlib.import_module("nex-nccl_amd.ring")
+    fn = ctypes.cast(oracle.lib().oracle_reduce_copy_fn, ctypes.c_void_p).value
+    x = [np.zeros(8, np.float32) for _ in range(2)]
+    with ring.RingComm(2, ring.HOST_MEMORY, 8 * 1024, fn) as comm:
+        for call in (lambda: comm.all_reduce_resident([a.ctypes.data for a in x], [a.ctypes.data for a in x], 8, 7, 0),
+                     lambda: comm.send_recv([a.ctypes.data for a in x], [1, 0], [a.ctypes.data for a in x], [1, 0], 4)):
+            with pytest.raises(nexr_pkg.NexrError) as e:
+                call()
+            assert e.value.code == nexr_pkg.Result.InvalidUsage
 
 
 def test_package_fails_loudly_without_library(nexr, monkeypatch, tmp_path):

@@ -40,15 +40,16 @@ def test_bench_extra_configs_and_c1():
                                        "c4_i8_max", "c4_i8_prod"}
     for v in d["extra_configs"].values():
         assert 0 < v["frac"] < 1
-    assert all(d["c1_ring"][k]["exact"] for k in ("device", "device_resident", "device_ll", "device_ll128", "host_staged",
-                                                       "cpu_oracle"))
-    assert d["resident_ring"]["exact"] and d["resident_ring"]["ms_per_call"] > 0
+    assert all(d["c1_ring"][k]["exact"] for k in ("device", "device_ll", "device_ll128", "host_staged", "cpu_oracle"))
+    assert d["c1_ring"]["device"]["step_wait"] == "word"  # both emulated ranks on the one GPU
+    assert "resident_ring" not in d and "device_resident" not in d["c1_ring"]  # extras: not in the default line
 
 
 def test_bench_fanout_rehearsal():
     d = _line([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-xgmi"],
               env={"NEXR_BENCH_FOLD": "1"})
     assert d["n_gpus"] == 2 and "c5" in d
+    assert d["phase_s"]["total"] < d["phase_s"]["cap_s"]
 
 
 def test_bench_torchrun_two_ranks():

@@ -219,7 +219,6 @@ def test_n1_line_carries_exact_and_per_set(monkeypatch, capsys):
     monkeypatch.setattr(torch.cuda, "set_device", lambda *a, **k: None)
     monkeypatch.setattr(bench, "DeviceWorkload", _FakeWorkload)
     monkeypatch.setattr(bench, "c1_ring", lambda: {"skipped": "test"})
-    monkeypatch.setattr(bench, "resident_ring", lambda: {"skipped": "test"})
     res = bench.main_ranks(_args(gpus=1, no_extra=False), bench.CONFIGS["c2"], _FakePkg())
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line == json.loads(json.dumps(res))
@@ -265,11 +264,18 @@ def test_check_exact_against_the_oracle_on_cpu_tensors(name):
         assert r2["exact"] is (not sampled), pos
 
 
+def _ring_result(cmd, exact=True, gpus=(0, 1)):
+    wait = cmd[cmd.index("--step-wait") + 1] if "--step-wait" in cmd else "default"
+    return {"gpus": list(gpus), "exact_all_ranks": exact, "step_wait": wait, "step_wait_in_effect": [wait],
+            "per_protocol_bytes": {"simple": {"4194304": {"ms": 0.1, "algbw_GBps": 41.9, "exact": exact}}}}
+
+
 def test_xgmi_probe_parts_link_rates_and_timeouts(monkeypatch, capsys):
     """N>1 with the xGMI probe on (faked: 4 GPUs, faked probe outputs): every part runs in its own
     bounded subprocess; the remote read/write and every ring result carry their rate against the
-    153 GB/s one-link bound next to their exact check; a part that times out is recorded as such and
-    the headline line is still printed."""
+    153 GB/s one-link bound next to their exact check; both process rings run under both step waits
+    (sync first, then the completion word) and the line carries both; a part that times out is
+    recorded as such and the headline line is still printed, with its phase times."""
     import torch
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
@@ -278,13 +284,13 @@ def test_xgmi_probe_parts_link_rates_and_timeouts(monkeypatch, capsys):
 
     def fake_bounded(cmd, timeout_s):
         arg = cmd[2]
-        seen.append((arg, timeout_s))
+        wait = cmd[cmd.index("--step-wait") + 1] if "--step-wait" in cmd else None
+        seen.append((arg, wait, timeout_s))
         if arg == "--peer-step":
             return {"gpus": [0, 1], "remote_read": {"xgmi_GBps": 76.5, "exact": True},
                     "remote_write": {"xgmi_GBps": 122.4, "exact": True}}
         if arg == "--ring-only":
-            return {"gpus": [0, 1], "exact_all_ranks": True,
-                    "per_protocol_bytes": {"simple": {"4194304": {"ms": 0.1, "algbw_GBps": 41.9, "exact": True}}}}
+            return _ring_result(cmd)
         if arg == "--resident-only":
             return {"ranks": 4, "ch1_4194304": {"ms": 0.2, "algbw_GBps": 20.0, "busbw_GBps": 30.0, "exact": True}}
         return {"error": f"timeout after {timeout_s:.0f} s"}  # --ring-all hangs
@@ -295,33 +301,106 @@ def test_xgmi_probe_parts_link_rates_and_timeouts(monkeypatch, capsys):
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["n_gpus"] == 4 and line["value"] > 0  # the headline is there
     x = line["xgmi_probe"]
-    assert [a for a, _ in seen] == ["--peer-step", "--ring-only", "--resident-only", "--ring-all"]
-    assert all(t <= 100 for _, t in seen)
+    assert [(a, w) for a, w, _ in seen] == [("--peer-step", None), ("--ring-only", "sync"), ("--ring-only", "word"),
+                                            ("--ring-all", "sync"), ("--ring-all", "word"), ("--resident-only", None)]
+    assert all(t <= 60 for _, _, t in seen)
     assert x["link_bound_GBps"] == 153.0
     assert x["remote_read"]["frac_of_link"] == pytest.approx(76.5 / 153, abs=1e-4)
     assert x["remote_write"]["frac_of_link"] == pytest.approx(122.4 / 153, abs=1e-4)
-    r = x["ring_processes"]["per_protocol_bytes"]["simple"]["4194304"]
-    assert r["busbw_GBps"] == pytest.approx(41.9, abs=0.01) and r["frac_of_link"] == pytest.approx(41.9 / 153, abs=1e-3)
+    for key in ("ring_processes", "ring_processes_word"):
+        r = x[key]["per_protocol_bytes"]["simple"]["4194304"]
+        assert r["busbw_GBps"] == pytest.approx(41.9, abs=0.01) and r["frac_of_link"] == pytest.approx(41.9 / 153, abs=1e-3)
+    assert x["ring_processes"]["step_wait"] == "sync" and x["ring_processes_word"]["step_wait"] == "word"
+    modes = x["step_wait_modes"]
+    assert modes["ring_processes"]["sync_exact_all_ranks"] is True and modes["ring_processes"]["word_exact_all_ranks"] is True
+    assert modes["visibility_fault"] is False and modes["link_or_schedule_fault"] is False
     assert x["resident_ring"]["ch1_4194304"]["frac_of_link"] == pytest.approx(30 / 153, abs=1e-3)
-    assert "timeout" in x["ring_processes_all_gpus"]["error"]
+    assert "timeout" in x["ring_processes_all_gpus"]["error"] and "timeout" in x["ring_processes_all_gpus_word"]["error"]
+    assert set(x["part_s"]) == {"peer_step", "ring_processes", "ring_processes_word", "ring_processes_all_gpus",
+                                "ring_processes_all_gpus_word", "resident_ring"}
+    ph = line["phase_s"]
+    for k in ("startup", "inputs", "timed_region", "solo_legs", "exact_checks", "xgmi_probe", "total"):
+        assert k in ph, k
+    assert ph["cap_s"] == bench.TOTAL_CAP_S
+
+
+@pytest.mark.parametrize("word_exact,sync_exact,visibility,link", [(False, True, True, False), (True, False, False, True),
+                                                                    (False, False, False, True)])
+def test_step_wait_verdict_tells_visibility_from_link_faults(monkeypatch, word_exact, sync_exact, visibility, link):
+    """The first multi-GPU line must tell a step-visibility fault (the completion word wrong, the
+    synchronisation right) from a link or schedule fault (the synchronisation wrong too)."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.delenv("NEXR_XGMI_RESIDENT", raising=False)
+
+    def fake_bounded(cmd, timeout_s):
+        if cmd[2] == "--peer-step":
+            return {"gpus": [0, 1]}
+        wait = cmd[cmd.index("--step-wait") + 1]
+        return _ring_result(cmd, exact=word_exact if wait == "word" else sync_exact,
+                            gpus=range(8) if cmd[2] == "--ring-all" else (0, 1))
+
+    monkeypatch.setattr(bench, "_bounded", fake_bounded)
+    res = bench.xgmi_probe()
+    m = res["step_wait_modes"]
+    assert m["visibility_fault"] is visibility and m["link_or_schedule_fault"] is link
+    assert m["ring_processes_all_gpus"]["word_exact_all_ranks"] is word_exact
+    assert m["ring_processes_all_gpus"]["sync_in_effect"] == ["sync"]
+
+
+def test_probe_budget_caps_the_line():
+    """The N > 1 line stays under TOTAL_CAP_S (300 s; the driver's BENCH timeout is 600 s): the probe
+    gets at most XGMI_BUDGET_S and never more than what the earlier phases left."""
+    assert bench.TOTAL_CAP_S <= 300 and bench.XGMI_BUDGET_S <= bench.TOTAL_CAP_S
+    assert bench.probe_budget(0.0) == bench.XGMI_BUDGET_S
+    assert bench.probe_budget(200.0) == pytest.approx(bench.TOTAL_CAP_S - bench.XGMI_MARGIN_S - 200.0)
+    assert bench.probe_budget(bench.TOTAL_CAP_S) == 0.0
+    for elapsed in (0.0, 60.0, 150.0, 280.0):
+        assert elapsed + bench.probe_budget(elapsed) <= bench.TOTAL_CAP_S
+
+
+def test_probe_parts_share_the_budget(monkeypatch):
+    """Every part that hangs is charged its whole limit (a faked clock): the parts together never
+    take more than the budget, and the ones that find it spent are recorded, not run."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.delenv("NEXR_XGMI_RESIDENT", raising=False)
+    clock = [1000.0]
+    monkeypatch.setattr(bench.time, "perf_counter", lambda: clock[0])
+    granted = []
+
+    def hang(cmd, timeout_s):
+        granted.append(timeout_s)
+        clock[0] += timeout_s
+        return {"gpus": [0, 1]} if cmd[2] == "--peer-step" else {"error": f"timeout after {timeout_s:.0f} s"}
+
+    monkeypatch.setattr(bench, "_bounded", hang)
+    budget = 120.0
+    res = bench.xgmi_probe(budget)
+    assert sum(granted) <= budget + 1e-6
+    assert res["wall_s"] <= budget
+    spent = [k for k in ("ring_processes_all_gpus", "ring_processes_all_gpus_word")
+             if "budget is spent" in res.get(k, {}).get("error", "")]
+    assert spent  # 45 + 40 + 40 = 125 > 120: the later parts were skipped
 
 
 def test_xgmi_probe_resident_parts_opt_in(monkeypatch):
     """Without NEXR_XGMI_RESIDENT=1 the probe runs only row f4's parts (the peer step and the
-    host-sequenced process rings); the frozen device-resident ring is not launched across GPUs."""
+    host-sequenced process rings); the device-resident ring (extras library) is not launched."""
     import torch
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     monkeypatch.delenv("NEXR_XGMI_RESIDENT", raising=False)
     seen = []
     monkeypatch.setattr(bench, "_bounded", lambda cmd, t: seen.append(cmd[2]) or {"gpus": [0, 1]})
     res = bench.xgmi_probe()
-    assert seen == ["--peer-step", "--ring-only", "--ring-all"] and "resident_ring" not in res
+    assert seen == ["--peer-step", "--ring-only", "--ring-only", "--ring-all", "--ring-all"]
+    assert "resident_ring" not in res
 
 
 def test_xgmi_probe_skipped_on_one_gpu(monkeypatch):
     import torch
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
     calls = []
-    monkeypatch.setattr(bench, "_bounded", lambda cmd, t: calls.append(cmd) or {"skipped": "needs 2 GPUs, found 1"})
+    monkeypatch.setattr(bench, "_bounded", lambda cmd, t: calls.append(cmd) or {})
     res = bench.xgmi_probe()
-    assert "skipped" in res and len(calls) == 1
+    assert "skipped" in res and calls == []

@@ -49,24 +49,32 @@ class Injector:
         return ctypes.cast(self.cb, ctypes.c_void_p).value
 
 
+def _comm(ring, kind, n, fn, timeout_ms):
+    """Send/recv lives in the opt-in extras library (include/nexr_extras.h): skipped when not built."""
+    extras = kind == "sendrecv"
+    if extras and not ring.extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in)")
+    return ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, fn, timeout_ms, 0, None, None, 2, extras=extras)
+
+
 def _run(comm, kind, n, count):
     x = [np.arange(count * n, dtype=np.uint32) + r for r in range(n)]
     o = [np.zeros(count * n, np.uint32) for _ in range(n)]
     xp, op = [v.ctypes.data for v in x], [v.ctypes.data for v in o]
     {"ring": lambda: comm.all_reduce(xp, op, count, U32, 0),
      "tree": lambda: comm.tree_all_reduce(xp, op, count, U32, 0),
-     "pat_rs": lambda: comm.pat_reduce_scatter(xp, op, count, U32, 0),
-     "pat_ag": lambda: comm.pat_all_gather(xp, op, count, U32),
+     "rs": lambda: comm.reduce_scatter(xp, op, count, U32, 0),
+     "ag": lambda: comm.all_gather(xp, op, count, U32),
      "sendrecv": lambda: comm.send_recv(xp, [(r + 1) % n for r in range(n)], op, [(r - 1) % n for r in range(n)],
                                         count * 4)}[kind]()
 
 
-@pytest.mark.parametrize("kind", ["ring", "tree", "pat_rs", "pat_ag", "sendrecv"])
+@pytest.mark.parametrize("kind", ["ring", "tree", "rs", "ag", "sendrecv"])
 @pytest.mark.parametrize("mode,code", [("fail", 1), ("stall", 3)])
 def test_step_failure_ends_every_rank(ring, oracle, nexr, kind, mode, code):
     n, count = 4, 20_000
     inj = Injector(oracle, at=5, mode=mode)
-    with ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, inj.address, 300, 0, None, None, 2) as comm:
+    with _comm(ring, kind, n, inj.address, 300) as comm:
         t0 = time.perf_counter()
         with pytest.raises(nexr.NexrError) as e:
             _run(comm, kind, n, count)
@@ -88,7 +96,7 @@ def test_healthy_comm_after_a_broken_one(ring, oracle):
         assert all(np.array_equal(v, np.arange(count, dtype=np.uint32) * 6) for v in o)
 
 
-@pytest.mark.parametrize("kind", ["ring", "tree", "pat_rs", "pat_ag", "sendrecv"])
+@pytest.mark.parametrize("kind", ["ring", "tree", "rs", "ag", "sendrecv"])
 @pytest.mark.parametrize("at", [1, 3])
 def test_thread_spawn_failure_returns_system_error(ring, oracle, nexr, kind, at, monkeypatch):
     """runThreads (nexr_ring.cpp) when the k-th rank thread cannot be created (test hook
@@ -97,7 +105,7 @@ def test_thread_spawn_failure_returns_system_error(ring, oracle, nexr, kind, at,
     cross the C entry point (std::terminate), and the communicator is marked broken."""
     n, count = 4, 20_000
     good = Injector(oracle, at=-1, mode="fail")
-    with ring.RingComm(n, ring.HOST_MEMORY, 8 * 1024, good.address, 20000, 0, None, None, 2) as comm:
+    with _comm(ring, kind, n, good.address, 20000) as comm:
         monkeypatch.setenv("NEXR_TEST_SPAWN_FAIL_AT", str(at))
         t0 = time.perf_counter()
         with pytest.raises(nexr.NexrError) as e:

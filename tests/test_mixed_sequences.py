@@ -1,9 +1,9 @@
 """Random sequences of every emulated collective on ONE communicator (CPU, the oracle serving every
-reduceCopy): ring AllReduce / ReduceScatter / AllGather / Reduce / Broadcast, tree AllReduce, PAT
-ReduceScatter / AllGather and grouped Send/Recv share links and step counters across calls, with
-different slice geometries (1-step and 2-step slices, PAT's unrounded steps), so every transition
-between them is exercised: round-up with credit return, FIFO wrap, step offsets. Integer sums make
-the expected result plain arithmetic, independent of fold order."""
+reduceCopy): ring AllReduce / ReduceScatter / AllGather / Reduce / Broadcast and tree AllReduce (and,
+with the opt-in extras library, grouped Send/Recv) share links and step counters across calls, with
+different slice geometries (1-step and 2-step slices), so every transition between them is
+exercised: round-up with credit return, FIFO wrap. Integer sums make the expected result plain
+arithmetic, independent of fold order."""
 import ctypes
 import importlib
 
@@ -22,7 +22,8 @@ def fn(oracle):
 
 
 U32 = 3
-KINDS = ("ar", "rs", "ag", "reduce", "bcast", "tree", "pat_rs", "pat_ag", "sendrecv")
+KINDS = ("ar", "rs", "ag", "reduce", "bcast", "tree")
+EXTRA_KINDS = ("sendrecv",)  # the opt-in extras library (include/nexr_extras.h)
 
 
 def _ptrs(arrs):
@@ -31,12 +32,16 @@ def _ptrs(arrs):
 
 @pytest.mark.parametrize("n,seed", [(2, 1), (2, 2), (2, 7), (3, 3), (3, 8), (4, 4), (4, 9), (5, 5), (6, 10), (7, 11), (8, 6),
                                     (13, 12)])
-def test_random_collective_sequences(ring, fn, n, seed):
+@pytest.mark.parametrize("extras", [False, True])
+def test_random_collective_sequences(ring, fn, n, seed, extras):
     rng = np.random.default_rng(seed)
     buff = int(rng.choice([8 * 2048, 8 * 4096, 8 * 8192]))
-    with ring.RingComm(n, ring.HOST_MEMORY, buff, fn, 30000, 0, None, None, 1 if n % 2 else 2) as comm:
+    if extras and not ring.extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in)")
+    kinds = KINDS + (EXTRA_KINDS if extras else ())
+    with ring.RingComm(n, ring.HOST_MEMORY, buff, fn, 30000, 0, None, None, 1 if n % 2 else 2, extras=extras) as comm:
         for step in range(40):
-            kind = KINDS[rng.integers(len(KINDS))]
+            kind = kinds[rng.integers(len(kinds))]
             count = int(rng.integers(1, 12_000))
             x = [rng.integers(0, 1 << 32, count * n, dtype=np.uint64).astype(np.uint32) for _ in range(n)]
             out = [np.full(count * n, 0xDEADBEEF, np.uint32) for _ in range(n)]
@@ -52,12 +57,12 @@ def test_random_collective_sequences(ring, fn, n, seed):
             elif kind == "tree":
                 comm.tree_all_reduce(_ptrs(x), _ptrs(out), count, U32, 0)
                 assert all(np.array_equal(o[:count], total[:count]) for o in out), what
-            elif kind in ("rs", "pat_rs"):
-                (comm.reduce_scatter if kind == "rs" else comm.pat_reduce_scatter)(_ptrs(x), _ptrs(out), count, U32, 0)
+            elif kind == "rs":
+                comm.reduce_scatter(_ptrs(x), _ptrs(out), count, U32, 0)
                 for r in range(n):
                     assert np.array_equal(out[r][:count], total[r * count:(r + 1) * count]), what
-            elif kind in ("ag", "pat_ag"):
-                (comm.all_gather if kind == "ag" else comm.pat_all_gather)(_ptrs(x), _ptrs(out), count, U32)
+            elif kind == "ag":
+                comm.all_gather(_ptrs(x), _ptrs(out), count, U32)
                 gathered = np.concatenate([v[:count] for v in x])
                 assert all(np.array_equal(o, gathered) for o in out), what
             elif kind == "reduce":

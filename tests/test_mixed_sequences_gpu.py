@@ -10,7 +10,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 U32 = 3
-KINDS = ("ar", "rs", "ag", "reduce", "bcast", "tree", "pat_rs", "pat_ag", "sendrecv")
+KINDS = ("ar", "rs", "ag", "reduce", "bcast", "tree")
+EXTRA_KINDS = ("sendrecv",)  # the opt-in extras library (include/nexr_extras.h)
 
 
 @pytest.fixture(scope="module")
@@ -20,12 +21,16 @@ def ring(nexr):
 
 
 @pytest.mark.parametrize("n,seed", [(2, 21), (3, 22), (4, 23), (8, 24)])
-def test_random_collective_sequences_device(ring, n, seed):
+@pytest.mark.parametrize("extras", [False, True])
+def test_random_collective_sequences_device(ring, n, seed, extras):
     rng = np.random.default_rng(seed)
     buff = int(rng.choice([8 * 4096, 8 * 16384, 1 << 20]))
-    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, tree_ranks_per_node=1 if n % 2 else 2) as comm:
+    if extras and not ring.extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in)")
+    kinds = KINDS + (EXTRA_KINDS if extras else ())
+    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, tree_ranks_per_node=1 if n % 2 else 2, extras=extras) as comm:
         for step in range(30):
-            kind = KINDS[rng.integers(len(KINDS))]
+            kind = kinds[rng.integers(len(kinds))]
             count = int(rng.integers(1, 200_000))
             xs = [rng.integers(0, 1 << 32, count * n, dtype=np.uint64).astype(np.uint32) for _ in range(n)]
             total = np.zeros(count * n, np.uint64)
@@ -42,12 +47,12 @@ def test_random_collective_sequences_device(ring, n, seed):
             if kind in ("ar", "tree"):
                 (comm.all_reduce if kind == "ar" else comm.tree_all_reduce)(xp, op, count, U32, 0)
                 assert all(np.array_equal(got(r)[:count], total[:count]) for r in range(n)), what
-            elif kind in ("rs", "pat_rs"):
-                (comm.reduce_scatter if kind == "rs" else comm.pat_reduce_scatter)(xp, op, count, U32, 0)
+            elif kind == "rs":
+                comm.reduce_scatter(xp, op, count, U32, 0)
                 for r in range(n):
                     assert np.array_equal(got(r)[:count], total[r * count:(r + 1) * count]), what
-            elif kind in ("ag", "pat_ag"):
-                (comm.all_gather if kind == "ag" else comm.pat_all_gather)(xp, op, count, U32)
+            elif kind == "ag":
+                comm.all_gather(xp, op, count, U32)
                 gathered = np.concatenate([v[:count] for v in xs])
                 assert all(np.array_equal(got(r), gathered) for r in range(n)), what
             elif kind == "reduce":

@@ -1,5 +1,5 @@
 """Host-code sanitizers (CPU only; GPU sanitizers are not available on this pool): the emulated
-collectives (nexr_ring.cpp, nexr_pat.cpp, nexr_p2p.cpp) and the C oracle built from source with g++ under ThreadSanitizer and under
+collectives (nexr_ring.cpp) and the C oracle built from source with g++ under ThreadSanitizer and under
 AddressSanitizer + UndefinedBehaviorSanitizer, driven by tests/native/ring_stress.cpp with oracle
 steps for the SIMPLE, LL and LL128 protocols, 2-6 rank threads, FIFO wrap-around."""
 import os
@@ -18,8 +18,7 @@ def test_ring_driver_under_sanitizer(tmp_path, san):
     exe = tmp_path / f"ring_stress_{san.split(',')[0]}"
     cmd = ["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={san}", "-fno-omit-frame-pointer", "-D__HIP_PLATFORM_AMD__",
            f"-I{HIP_INC}", os.path.join(ROOT, "tests", "native", "ring_stress.cpp"),
-           os.path.join(ROOT, "tests", "native", "resident_stubs.cpp"),  # the resident kernels are device code
-           *[os.path.join(ROOT, "nex-nccl_amd", "csrc", f"{f}.cpp") for f in ("nexr_ring", "nexr_pat", "nexr_p2p")],
+           os.path.join(ROOT, "nex-nccl_amd", "csrc", "nexr_ring.cpp"),
            "-x", "c", "-std=c11",
            os.path.join(ROOT, "oracle", "nexr_oracle.c"), "-x", "none",
            f"-L{os.path.join(ROOT, 'nex-nccl_amd')}", "-lnexr", f"-Wl,-rpath,{os.path.join(ROOT, 'nex-nccl_amd')}",

@@ -24,6 +24,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "peer_ring_worker.py")
 
 
+def ring_extras_available() -> bool:
+    import importlib
+    return importlib.import_module("nex-nccl_amd.ring").extras_available()
+
+
 def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="allreduce", root=0):
     name = f"/nexr_test_{uuid.uuid4().hex[:16]}"
     out = [str(tmp_path / f"rank{r}") for r in range(n)]
@@ -52,9 +57,14 @@ def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="al
         if os.path.exists(shm_path):
             os.unlink(shm_path)
     # Every rank ran on GPU rank mod (visible GPUs): distinct GPUs for neighbours whenever there are two.
+    # The step wait in effect is the completion word only when every rank shares one GPU, the stream
+    # synchronisation otherwise (nexrRingCommGetStepWait), unless NEXR_STEP_WAIT forces one.
     for r in range(n):
-        ordinal, n_vis = map(int, open(f"{out[r]}.device").read().split())
+        ordinal, n_vis, wait = open(f"{out[r]}.device").read().split()
+        ordinal, n_vis = int(ordinal), int(n_vis)
         assert ordinal == r % n_vis, (r, ordinal, n_vis)
+        forced = os.environ.get("NEXR_STEP_WAIT")
+        assert wait == (forced if forced in ("word", "sync") else "word" if n_vis == 1 or n == 1 else "sync"), (r, wait)
     return [[np.load(f"{out[r]}.{c}.npy") for c in range(calls)] for r in range(n)]
 
 
@@ -86,6 +96,8 @@ def test_peer_ring_resident_processes(oracle, tmp_path, n, dt, op):
     launch; the launches of different processes meet only through the FIFOs and the step records
     behind them, mapped over IPC (on one GPU the ranks' kernels run side by side on it). Two calls,
     the second in place: equal to the fold-order oracle, as the host-sequenced process ring is."""
+    if not ring_extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in: make -C nex-nccl_amd/csrc EXTRAS=1)")
     from oracle.ring import ring_allreduce_expected
     count, buff = 200_003, 1 << 18
     outs = _run_ring(tmp_path, n, dt, op, count, 0, buff, coll="allreduce_resident")
@@ -104,6 +116,8 @@ def test_peer_ring_alternating_host_and_resident(oracle, tmp_path, n, dt, op):
     the previous result: every switch waits until the next rank has consumed what the other form sent
     (ringLinkHandover, nexr_ring.cpp), so no slot is overwritten before it is read. Each call equals
     the fold-order oracle of its input."""
+    if not ring_extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in: make -C nex-nccl_amd/csrc EXTRAS=1)")
     from oracle.ring import ring_allreduce_expected
     count, buff, calls = 200_003, 1 << 18, 4
     outs = _run_ring(tmp_path, n, dt, op, count, 0, buff, calls=calls, coll="allreduce_mixed")
@@ -150,35 +164,12 @@ def test_peer_ring_other_collectives(oracle, tmp_path, coll, n, dt, op, proto, r
             assert mg.canon_bytes(dt, outs[r][c]) == mg.canon_bytes(dt, exp[r]), f"rank {r}, call {c}"
 
 
-@pytest.mark.parametrize("n,dt,op", [(2, mg.F32, 0), (3, mg.BF16, 0), (4, mg.I32, 2), (5, mg.F16, 1)])
-def test_peer_pat_reduce_scatter_processes(oracle, tmp_path, n, dt, op):
-    """PAT ReduceScatter with one process per rank: the r -/+ 2^d links are IPC-mapped FIFOs."""
-    from oracle import pat
-    count, buff = 30_001, 1 << 16
-    outs = _run_ring(tmp_path, n, dt, op, count, 0, buff, calls=2, coll="pat_rs")
-    inputs = mg.gen_inputs(dt, n, count * n, 7, special=True)
-    dev_op, arg = oracle.host_to_dev_red_op(op, dt, n)
-    exp = pat.reduce_scatter_expected(inputs, dt, dev_op, arg, buff // 8)
-    for r in range(n):
-        for c in range(2):
-            assert mg.canon_bytes(dt, outs[r][c]) == mg.canon_bytes(dt, exp[r]), f"rank {r}, call {c}"
-
-
-@pytest.mark.parametrize("n", [2, 3, 4, 6])
-def test_peer_pat_all_gather_processes(tmp_path, n):
-    count = 20_011
-    outs = _run_ring(tmp_path, n, mg.F16, 0, count, 0, 1 << 15, calls=2, coll="pat_ag")
-    inputs = mg.gen_inputs(mg.F16, n, count, 7, special=True)
-    exp = np.concatenate(inputs).tobytes()
-    for r in range(n):
-        for c in range(2):
-            assert outs[r][c].tobytes() == exp, f"rank {r}, call {c}"
-
-
 @pytest.mark.parametrize("n,count", [(2, 300_007), (3, 300_007), (4, 300_007), (3, 1_001)])
 def test_peer_send_recv_processes(tmp_path, n, count):
     """Send/Recv with one process per rank: call c shifts by c+1 (a local copy when it wraps to 0);
     4,004-byte messages take the LL links."""
+    if not ring_extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in: make -C nex-nccl_amd/csrc EXTRAS=1)")
     calls = n + 1
     outs = _run_ring(tmp_path, n, mg.I32, 0, count, 0, 1 << 16, calls=calls, coll="sendrecv")
     inputs = mg.gen_inputs(mg.I32, n, count, 7, special=True)

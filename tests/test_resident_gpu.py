@@ -19,7 +19,8 @@ SUM, PROD, MAX, MIN, AVG = 0, 1, 2, 3, 4
 @pytest.fixture(scope="module")
 def ring(nexr):
     assert torch.cuda.is_available()
-    return importlib.import_module("nex-nccl_amd.ring")
+    from conftest import extras_ring
+    return extras_ring()  # include/nexr_extras.h: skipped when the opt-in library is not built
 
 
 def _dev(arrs):
@@ -144,7 +145,7 @@ def test_resident_across_gpus(ring, oracle):
         assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), r
 
 
-def test_resident_uncached_layout_in_a_fresh_process():
+def test_resident_uncached_layout_in_a_fresh_process(ring):
     """NEXR_RESIDENT_UNCACHED=1 gives a one-GPU communicator the layout used when ranks span GPUs
     (uncached FIFOs and step records, hipDeviceMallocUncached): the C1 shape and a 4-rank, 2-channel
     bf16 case stay exact. Run in a child process: the switch is read once per process."""
@@ -163,7 +164,7 @@ for n, dt, count, buff, nch in ((2, mg.F32, 1 << 20, 0, 1), (4, mg.BF16, 300_001
     send = [torch.from_numpy(a.copy()).cuda() for a in inputs]
     recv = [torch.zeros_like(s) for s in send]
     torch.cuda.synchronize()
-    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000) as comm:
+    with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000, extras=True) as comm:
         for _ in range(3):
             comm.all_reduce_resident([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, dt, 0)
     exp = ring_allreduce_expected(inputs, dt, 0, buff or (4 << 20), nch)
@@ -244,7 +245,7 @@ def test_resident_reduce_and_broadcast(ring, oracle, n, root, dt, op, nch):
         assert mg.canon_bytes(dt, bc_in_place[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), f"all-reduce rank {r}"
 
 
-def test_resident_team_shrinks_to_kernel_occupancy():
+def test_resident_team_shrinks_to_kernel_occupancy(ring):
     """NEXR_RESIDENT_TEAM=128 with 8 ranks x 2 channels asks for 2,048 workgroups of the int8 kernel
     on one GPU, more than its occupancy lets be resident at once: the team shrinks to fit
     (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs) instead of waiting on workgroups that cannot
@@ -264,7 +265,7 @@ inputs = mg.gen_inputs(dt, n, count, 41, special=True)
 send = [torch.from_numpy(a.copy()).cuda() for a in inputs]
 recv = [torch.zeros_like(s) for s in send]
 torch.cuda.synchronize()
-with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000) as comm:
+with ring.RingComm(n, ring.DEVICE_MEMORY, buff, n_channels=nch, timeout_ms=20000, extras=True) as comm:
     comm.all_reduce_resident([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, dt, 2)
 exp = ring_allreduce_expected(inputs, dt, 2, buff, nch)
 assert all(mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]) for r in range(n))

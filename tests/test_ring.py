@@ -171,12 +171,14 @@ def test_ring_with_reference_execution_steps(ring, oracle, n_ranks, dt, op, spec
 
 
 def test_resident_all_reduce_needs_device_memory(ring, oracle_fn):
-    """nexrRingAllReduceResident runs only on device-memory SIMPLE communicators: a host-memory one
+    """(extras library) nexrRingAllReduceResident runs only on device-memory SIMPLE communicators: a host-memory one
     (here with the CPU oracle as its step, so no GPU is touched) is rejected with InvalidUsage before any
     HIP call, and the communicator stays usable."""
     x = [np.arange(100, dtype=np.float32) + r for r in range(2)]
     y = [np.zeros(100, np.float32) for _ in range(2)]
-    with ring.RingComm(2, ring.HOST_MEMORY, 64 << 10, oracle_fn, timeout_ms=20000) as comm:
+    if not ring.extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in: make -C nex-nccl_amd/csrc EXTRAS=1)")
+    with ring.RingComm(2, ring.HOST_MEMORY, 64 << 10, oracle_fn, timeout_ms=20000, extras=True) as comm:
         with pytest.raises(ring.NexrError) as e:
             comm.all_reduce_resident([a.ctypes.data for a in x], [b.ctypes.data for b in y], 100, mg.F32, 0)
         assert e.value.code == 5  # ncclInvalidUsage

@@ -25,6 +25,8 @@ def test_probe_skips_without_two_gpus():
 
 def test_bench_wrapper_reports_failures(monkeypatch):
     import bench
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)  # the probe's parts run only with 2+ GPUs
 
     class Boom:
         pid = 999_999_999

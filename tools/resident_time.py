@@ -39,7 +39,7 @@ def main():
                 torch.cuda.synchronize()
                 sp, rp = [x.data_ptr() for x in xs], [y.data_ptr() for y in ys]
                 line = {"ranks": n, "channels": nch, "bytes_per_rank": nbytes}
-                with ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=20000) as comm:
+                with ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=20000, extras=True) as comm:
                     pair = ((("resident", comm.tree_all_reduce_resident), ("host", comm.tree_all_reduce)) if args.tree
                             else (("resident", comm.all_reduce_resident), ("host", comm.all_reduce)))
                     line["algorithm"] = "tree" if args.tree else "ring"
@@ -71,7 +71,7 @@ def other_colls(ring, n, nch, count, iters):
     big = [torch.arange(count * n, dtype=torch.float32, device="cuda").remainder_(1000) + r for r in range(n)]
     small = [torch.empty(count, dtype=torch.float32, device="cuda") for _ in range(n)]
     torch.cuda.synchronize()
-    with ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=20000) as comm:
+    with ring.RingComm(n, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=20000, extras=True) as comm:
         calls = {"reduce_scatter": lambda: comm.reduce_scatter_resident([b.data_ptr() for b in big],
                                                                         [s.data_ptr() for s in small], count, 7, 0),
                  "all_gather": lambda: comm.all_gather_resident([s.data_ptr() for s in small],

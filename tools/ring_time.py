@@ -29,7 +29,7 @@ def run(n, mode_name, proto_name, coll, iters):
     rng = np.random.default_rng(n)
     # small integers: every sum order gives the same fp32 result, so numpy checks the schedule
     x = [rng.integers(-1000, 1000, count * n).astype(np.float32) for _ in range(n)]
-    out_n = count * n if coll in ("allgather", "pat_ag") else count
+    out_n = count * n if coll == "allgather" else count
     if coll == "sendrecv":  # ring shift of the first 4 MiB of every rank's input
         x = [v[:count].copy() for v in x]
     if mode == ring.DEVICE_MEMORY:
@@ -47,13 +47,11 @@ def run(n, mode_name, proto_name, coll, iters):
     fns = ORACLE_FNS if mode_name == "cpu-oracle" else (None, None, None)
     kw = dict(protocol=proto, ll_fn_address=fns[1], ll128_fn_address=fns[2], tree_ranks_per_node=1,
               n_channels=int(os.environ.get("RING_TIME_CHANNELS", "1")))
-    with ring.RingComm(n, mode, 0, fns[0], **kw) as comm:
+    with ring.RingComm(n, mode, 0, fns[0], extras=coll == "sendrecv", **kw) as comm:
         call = {"allreduce": lambda: comm.all_reduce(sp, rp, count, F32, 0),
                 "tree": lambda: comm.tree_all_reduce(sp, rp, count, F32, 0),
                 "reducescatter": lambda: comm.reduce_scatter(sp, rp, count, F32, 0),
                 "allgather": lambda: comm.all_gather(sp, rp, count, F32),
-                "pat_rs": lambda: comm.pat_reduce_scatter(sp, rp, count, F32, 0),
-                "pat_ag": lambda: comm.pat_all_gather(sp, rp, count, F32),
                 "sendrecv": lambda: comm.send_recv(sp, [(r + 1) % n for r in range(n)], rp,
                                                    [(r - 1) % n for r in range(n)], count * 4)}[coll]
         call()
@@ -64,7 +62,7 @@ def run(n, mode_name, proto_name, coll, iters):
     got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
     if coll in ("allreduce", "tree"):
         exp = [sum(v[:count] for v in x)] * n
-    elif coll in ("reducescatter", "pat_rs"):
+    elif coll == "reducescatter":
         exp = [sum(v[k * count:(k + 1) * count] for v in x) for k in range(n)]
     elif coll == "sendrecv":
         exp = [x[(r - 1) % n] for r in range(n)]
@@ -83,7 +81,7 @@ for n in [int(v) for v in os.environ.get("RING_TIME_RANKS", "2,4").split(",")]:
             continue
         for proto_name in protos:
             colls = ("allreduce", "tree", "reducescatter", "allgather")
-            for coll in colls + (("pat_rs", "pat_ag", "sendrecv") if proto_name == "simple" else ()):
+            for coll in colls + (("sendrecv",) if proto_name == "simple" and ring.extras_available() else ()):
                 iters = 3 if mode_name == "cpu-oracle" else 10
                 dt = run(n, mode_name, proto_name, coll, iters)
                 print(f"{n:>5} {mode_name:<10} {proto_name:<6} {coll:<14} {dt * 1e3:9.3f} {count * 4 / dt / 1e9:11.2f}",

@@ -13,10 +13,15 @@ fp32 sum, 256 MiB per buffer. Then the process-rank ring itself across the two G
 SIMPLE; LL and LL128 at 4 MiB) with every step's reduce-copy writing into the peer GPU's HBM over
 xGMI; every rank's result is checked exactly (integer-valued inputs). `--ring-all N` runs the same
 ring with N processes on the first N GPUs; `--peer-step` runs only the three kernel legs (bench.py
-runs each part as its own bounded subprocess). Prints one JSON line; with fewer than two GPUs it prints a
+runs each part as its own bounded subprocess). `--step-wait sync|word` sets NEXR_STEP_WAIT for the
+ring's ranks: how each rank thread waits for its step before posting it (stream synchronisation, the
+cross-GPU default, or the completion word); each rank reports the wait in effect, and bench.py runs
+both so that a step-visibility fault (word wrong, sync right) is told apart from a link fault. Prints one JSON line; with fewer than two GPUs it prints a
 "skipped" line and exits 0. bench.py runs it as bounded subprocesses when it drives more than one
 GPU, so a failure here can never take the bench line down with it.
 """
+from __future__ import annotations
+
 import ctypes
 import importlib
 import json
@@ -117,7 +122,7 @@ def resident_ring(n_ranks: int, sizes=(1 << 22, 1 << 26, 1 << 28), channels=(1, 
             ys = [torch.empty_like(x) for x in xs]
             for d in range(min(nd, n_ranks)):
                 torch.cuda.synchronize(d)
-            with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=10000) as comm:
+            with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 0, n_channels=nch, timeout_ms=10000, extras=True) as comm:
                 comm.all_reduce_resident([x.data_ptr() for x in xs], [y.data_ptr() for y in ys], count, 7, 0)
                 iters = 10
                 t0 = time.perf_counter()
@@ -134,7 +139,7 @@ def resident_ring(n_ranks: int, sizes=(1 << 22, 1 << 26, 1 << 28), channels=(1, 
 
 
 PROTOCOLS = {"simple": 0, "ll": 1, "ll128": 2}
-if os.environ.get("NEXR_XGMI_RESIDENT") == "1":  # frozen, beyond SURVEY §8: opt-in
+if os.environ.get("NEXR_XGMI_RESIDENT") == "1":  # beyond SURVEY §8: opt-in, needs the extras library
     PROTOCOLS["simple_resident"] = 0  # nexrPeerRingAllReduceResident
 LL_COUNT = 1 << 20  # the LL protocols run C1's 4 MiB only (they move 2x / 16/15x the payload)
 
@@ -149,10 +154,12 @@ def ring_rank(rank: int, n_ranks: int, shm: str, counts) -> int:
     torch.cuda.set_device(dev)
     ring = importlib.import_module("nex-nccl_amd.ring")
     out = {}
+    waits = {}
     for pname, proto in PROTOCOLS.items():
         out[pname] = res = {}
         with ring.PeerRingComm(n_ranks, rank, f"{shm}_{pname}", device=dev, protocol=proto,
-                               timeout_ms=30000) as comm:
+                               timeout_ms=30000, extras=pname == "simple_resident") as comm:
+            waits[pname] = comm.step_wait()
             call = comm.all_reduce_resident if pname == "simple_resident" else comm.all_reduce
             for count in (counts if pname.startswith("simple") else [LL_COUNT]):
                 x = torch.arange(count, dtype=torch.float32, device=f"cuda:{dev}").remainder_(1000) + rank
@@ -168,11 +175,12 @@ def ring_rank(rank: int, n_ranks: int, shm: str, counts) -> int:
                 dt = (time.perf_counter() - t0) / iters
                 res[str(count * 4)] = {"ms": round(dt * 1e3, 3), "algbw_GBps": round(count * 4 / dt / 1e9, 2),
                                        "exact": bool(torch.equal(y, exp))}
-    print(json.dumps({"rank": rank, "gpu": dev, "results": out}), flush=True)
+    print(json.dumps({"rank": rank, "gpu": dev, "step_wait": waits, "results": out}), flush=True)
     return 0
 
 
-def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "1048576,16777216"):
+def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "1048576,16777216",
+                   step_wait: str | None = None):
     """n_ranks child processes, rank r on GPU r mod visible, each mapping its successor's FIFO over IPC:
     the ring all-reduce at C1's 4 MiB (SIMPLE, LL, LL128) and 64 MiB (SIMPLE). Reports rank 0's timing
     and whether EVERY rank's output was exact. Children stay in this process's group, so a caller
@@ -180,9 +188,12 @@ def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "104
     import subprocess
     import uuid
     shm = f"/nexr_xgmi_{uuid.uuid4().hex[:12]}"
+    env = dict(os.environ)
+    if step_wait:
+        env["NEXR_STEP_WAIT"] = step_wait
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--ring-rank", str(r), "--ranks",
                                str(n_ranks), "--shm", shm, "--counts", counts], stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(n_ranks)]
+                              stderr=subprocess.PIPE, text=True, env=env) for r in range(n_ranks)]
     outs = []
     try:
         for p in procs:
@@ -192,17 +203,20 @@ def ring_processes(n_ranks: int = 2, timeout_s: float = 60.0, counts: str = "104
             if p.poll() is None:
                 p.kill()
                 p.wait()
-        return {"error": "timeout", "ranks": n_ranks}
+        return {"error": "timeout", "ranks": n_ranks, "step_wait": step_wait or "default"}
     finally:
         for pname in PROTOCOLS:
             if os.path.exists(f"/dev/shm{shm}_{pname}"):
                 os.unlink(f"/dev/shm{shm}_{pname}")
     if any(p.returncode != 0 for p in procs):
-        return {"error": [p.returncode for p in procs], "stderr": [e[-300:] for _, e in outs]}
+        return {"error": [p.returncode for p in procs], "stderr": [e[-300:] for _, e in outs],
+                "step_wait": step_wait or "default"}
     lines = [json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]) for o, _ in outs]
     r0 = lines[0]["results"]
     exact_all = all(v["exact"] for ln in lines for proto in ln["results"].values() for v in proto.values())
     return {"per_protocol_bytes": r0, "exact_all_ranks": exact_all, "gpus": [ln["gpu"] for ln in lines],
+            "step_wait": step_wait or "default",
+            "step_wait_in_effect": sorted({w for ln in lines for w in ln.get("step_wait", {}).values()}),
             "ranks": f"{n_ranks} processes, rank r on GPU r, fp32 sum; SIMPLE at 4 and 64 MiB (and the "
                      "device-resident form with NEXR_XGMI_RESIDENT=1), LL and LL128 at 4 MiB; "
                      "timings of rank 0"}
@@ -213,13 +227,15 @@ if __name__ == "__main__":
     if "--resident-only" in a:  # rehearsal of the resident ring alone: --resident-only N
         print(json.dumps(resident_ring(int(a[a.index("--resident-only") + 1]))), flush=True)
         sys.exit(0)
-    if "--ring-only" in a:  # rehearsal of the two-rank process ring alone (any number of GPUs)
-        print(json.dumps(ring_processes()), flush=True)
+    wait = a[a.index("--step-wait") + 1] if "--step-wait" in a else None
+    if "--ring-only" in a:  # the two-rank process ring alone (any number of GPUs)
+        print(json.dumps(ring_processes(step_wait=wait,
+                                        timeout_s=float(os.environ.get("NEXR_RING_ONLY_TIMEOUT", "35")))), flush=True)
         sys.exit(0)
     if "--ring-all" in a:  # the process ring over the first N GPUs (bench.py at N >= 3)
         n = int(a[a.index("--ring-all") + 1])
-        print(json.dumps(ring_processes(n, timeout_s=float(os.environ.get("NEXR_RING_ALL_TIMEOUT", "75")))),
-              flush=True)
+        print(json.dumps(ring_processes(n, timeout_s=float(os.environ.get("NEXR_RING_ALL_TIMEOUT", "50")),
+                                        step_wait=wait)), flush=True)
         sys.exit(0)
     if "--ring-rank" in a:
         sys.exit(ring_rank(int(a[a.index("--ring-rank") + 1]), int(a[a.index("--ranks") + 1]),
