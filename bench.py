@@ -211,7 +211,7 @@ class DeviceWorkload:
         sp, dp, _, _ = self.sets[i % len(self.sets)]
         return self.pkg.make_work(sp, dp, self.n, self.cfg["arg"])
 
-    def per_set(self, rounds: int = 6) -> dict:
+    def per_set(self, rounds: int = 12) -> dict:
         """After the timed region (and after check_exact: it overwrites the outputs): `rounds` x sets
         more launches, round-robin over the sets as in the timed loop, with HIP events around every
         launch on the launch stream; the average kernel time of each set and where its buffers sit

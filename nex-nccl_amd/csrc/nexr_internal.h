@@ -138,5 +138,10 @@ __host__ __device__ constexpr int unroll_for(int dt, int k, int pol) {
                                                                 : 4;
 }
 __host__ __device__ constexpr int block_for(int dt, int k, int pol) { return kTripPacks / unroll_for(dt, k, pol); }
+// Load / store order inside a trip (nexr_kernels.hip body()): source-major (every source's pack u = 0,
+// then u = 1, ...; all packs stored after the last fold). Pack-major (pack by pack, each stored after
+// its fold) was 0.5-2.6 % slower on C2, C4 and the other U > 1 geometries, byte-identical
+// (tools/pack_order_ab.hip, profiles/r04b_pack_order_ab_not_kept.txt); the switch stays for that harness.
+__host__ __device__ constexpr bool pack_major_for(int, int, int) { return false; }
 
 }  // namespace nexr

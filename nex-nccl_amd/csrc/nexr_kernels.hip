@@ -46,7 +46,7 @@ __device__ __forceinline__ void do_element(const char* const (&src)[K], char* co
 
 // `bid`/`nblk`: this workgroup's index among the `nblk` workgroups working on `p` (the whole grid
 // for a single launch; a slice of it for a batch launch).
-template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
+template <int D, int OP, int K, int POL, bool IsMin, int U, int B, bool PM>
 __device__ __forceinline__ void body(const RCParams& p, uint64_t bid, uint64_t nblk) {
   using T = Ty<D>;
   constexpr int esz = 16 / T::EPP;
@@ -86,22 +86,39 @@ __device__ __forceinline__ void body(const RCParams& p, uint64_t bid, uint64_t n
   const uint64_t nPacks = p.nPacks;
   const uint64_t nFull = nPacks / (B * U);  // groups of B*U packs
   uint64_t g = bid;
-  // Full groups: K*U 16-B loads in flight per lane, then the fold, then M*U stores.
+  // Full groups: K*U 16-B loads in flight per lane, then the fold, then M*U stores. PM (pack-major)
+  // issues the loads pack by pack (pack u of every source before pack u + 1 of any) and stores each
+  // pack right after its fold, so pack 0 folds and leaves while pack 1's loads are still arriving;
+  // otherwise source by source, and every pack is stored after the last fold.
   for (; g < nFull; g += nblk) {
     const uint64_t off = (g * (B * U) + threadIdx.x) * 16;
     u32x4 in[U][K];
+    if constexpr (PM) {
 #pragma unroll
-    for (int s = 0; s < K; s++)
+      for (int u = 0; u < U; u++)
 #pragma unroll
-      for (int u = 0; u < U; u++) in[u][s] = ld16<POL>(src[s] + off + u * B * 16);
-    u32x4 out[U];
+        for (int s = 0; s < K; s++) in[u][s] = ld16<POL>(src[s] + off + u * B * 16);
 #pragma unroll
-    for (int u = 0; u < U; u++) out[u] = f.run(in[u]);
+      for (int u = 0; u < U; u++) {
+        const u32x4 out = f.run(in[u]);
 #pragma unroll
-    for (int d = 0; d < NEXR_MAX_DSTS; d++) {
-      if (d < nDsts) {
+        for (int d = 0; d < NEXR_MAX_DSTS; d++)
+          if (d < nDsts) st16<POL>(dst[d] + off + u * B * 16, out);
+      }
+    } else {
 #pragma unroll
-        for (int u = 0; u < U; u++) st16<POL>(dst[d] + off + u * B * 16, out[u]);
+      for (int s = 0; s < K; s++)
+#pragma unroll
+        for (int u = 0; u < U; u++) in[u][s] = ld16<POL>(src[s] + off + u * B * 16);
+      u32x4 out[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) out[u] = f.run(in[u]);
+#pragma unroll
+      for (int d = 0; d < NEXR_MAX_DSTS; d++) {
+        if (d < nDsts) {
+#pragma unroll
+          for (int u = 0; u < U; u++) st16<POL>(dst[d] + off + u * B * 16, out[u]);
+        }
       }
     }
   }
@@ -117,19 +134,20 @@ __device__ __forceinline__ void body(const RCParams& p, uint64_t bid, uint64_t n
   }
 }
 
-template <int D, int OP, int K, int POL, int U, int B>
+template <int D, int OP, int K, int POL, int U, int B, bool PM = pack_major_for(D, K, POL)>
 __device__ __forceinline__ void dispatch_minmax(const RCParams& p, uint64_t bid, uint64_t nblk) {
   if constexpr (OP == nexrDevMinMax) {
-    if ((p.redArg & 1) == 0) body<D, OP, K, POL, true, U, B>(p, bid, nblk);  // isMin = (arg&1)==0, reduce_kernel.h:64
-    else body<D, OP, K, POL, false, U, B>(p, bid, nblk);
+    if ((p.redArg & 1) == 0) body<D, OP, K, POL, true, U, B, PM>(p, bid, nblk);  // isMin = (arg&1)==0, reduce_kernel.h:64
+    else body<D, OP, K, POL, false, U, B, PM>(p, bid, nblk);
   } else {
-    body<D, OP, K, POL, false, U, B>(p, bid, nblk);
+    body<D, OP, K, POL, false, U, B, PM>(p, bid, nblk);
   }
 }
 
-template <int D, int OP, int K, int POL, int U = unroll_for(D, K, POL), int B = block_for(D, K, POL)>
+template <int D, int OP, int K, int POL, int U = unroll_for(D, K, POL), int B = block_for(D, K, POL),
+          bool PM = pack_major_for(D, K, POL)>
 __global__ __launch_bounds__(B) void reduce_copy_kernel(RCParams p) {
-  dispatch_minmax<D, OP, K, POL, U, B>(p, blockIdx.x, gridDim.x);
+  dispatch_minmax<D, OP, K, POL, U, B, PM>(p, blockIdx.x, gridDim.x);
 }
 
 // Batch launch (the analogue of a kernel running a ncclDevWorkBatch: src/device/common.h:307-342):

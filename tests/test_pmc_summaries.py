@@ -53,7 +53,7 @@ def test_traffic_tool_counts_only_the_configs_instantiation(tmp_path):
 
 
 def test_ll_step_traffic_summary_reproduces_from_the_committed_counters():
-    """profiles/r02s5_ll_pmc.txt (DESIGN §4b) is rebuilt from the committed counter collections by
+    """profiles/r02s5_ll_pmc.txt (DESIGN §4.5) is rebuilt from the committed counter collections by
     tools/ll_prof_summary.py, and every LL / LL128 / SIMPLE step moves its algorithmic bytes once."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import ll_prof_summary

@@ -5,7 +5,7 @@
 // carry three bits — sc0, sc1, nt — and MI355X_MICROARCH.md (stores of each flavour) says plain /
 // sc0 / nt stores KEEP the line in the XCD's L2 while sc1 / sc0 sc1 DROP it (write-through). Does
 // any other combination move the HBM rate of the write stream (the K = 8 configurations lose ~10 %
-// to the read/write mix) or of the read streams?
+// to the read/write mix, DESIGN §6.3 (docs/HISTORY.md §6)) or of the read streams?
 //
 // Each variant is the production trip (same geometry: unroll_for / block_for, one-shot grid, same
 // fold: Fold<> from nexr_kernels.hip) with either the stores or the loads issued as

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Allocation kind vs reduce-copy rate (diagnostic for the per-set spread).
+"""Allocation kind vs reduce-copy rate (diagnostic for the per-set spread, DESIGN §6.3 (docs/HISTORY.md §6) round 3).
 
 The placement probe (tools/placement_probe.py) found a per-allocation cost that no pointer shift
 inside an allocation moves. If that cost is how fragmented the physical memory behind an

@@ -1,5 +1,5 @@
 // What one emulated ring step costs the host, by the way it waits for the step's reduce-copy
-// (diagnostic for DESIGN §8: "one launch plus hipStreamSynchronize of a 128 KiB-2 MiB reduce-copy costs
+// (diagnostic for DESIGN §8.1: "one launch plus hipStreamSynchronize of a 128 KiB-2 MiB reduce-copy costs
 // 12.0-12.5 us"). Each iteration launches one nexrReduceCopy (fp32 sum, K = 2, M = 2: the ring's
 // recvReduceCopySend shape) on a non-blocking stream and waits for it with:
 //   sync       hipStreamSynchronize

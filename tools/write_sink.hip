@@ -1,4 +1,4 @@
-// Where does the write stream's cost arise? (diagnostic for DESIGN §6: 8 read streams alone stream at
+// Where does the write stream's cost arise? (diagnostic for DESIGN §6.3 (docs/HISTORY.md §6): 8 read streams alone stream at
 // ~6.6-6.8 TB/s, with one write stream beside them at ~5.9-6.05.) S read streams (fold = xor), then the
 // write stream in one of these forms:
 //   none        no store (the fold is kept live by a never-taken store)
