@@ -184,3 +184,26 @@ def test_resident_all_reduce_needs_device_memory(ring, oracle_fn):
         assert e.value.code == 5  # ncclInvalidUsage
         comm.all_reduce([a.ctypes.data for a in x], [b.ctypes.data for b in y], 100, mg.F32, 0)
     assert all(np.array_equal(b, x[0] + x[1]) for b in y)
+
+
+def test_step_wait_choice_without_a_gpu(ring, oracle_fn):
+    """nexrRingCommGetStepWait on communicators that never touch HIP (CPU checker steps): every rank on
+    device 0, so the completion word is the choice unless NEXR_STEP_WAIT forces one; the variable is
+    read once per process (fresh interpreters here)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import ctypes, importlib, json, sys; sys.path.insert(0, %r); import oracle; "
+            "ring = importlib.import_module('nex-nccl_amd.ring'); "
+            "fn = ctypes.cast(oracle.lib().oracle_reduce_copy_fn, ctypes.c_void_p).value; "
+            "c = ring.RingComm(3, ring.HOST_MEMORY, 0, fn); print(json.dumps(c.step_wait())); c.close()" % root)
+    for env_val, expect in ((None, "word"), ("sync", "sync"), ("word", "word"), ("bogus", "word")):
+        env = dict(os.environ)
+        env.pop("NEXR_STEP_WAIT", None)
+        if env_val:
+            env["NEXR_STEP_WAIT"] = env_val
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr[-1500:]
+        assert json.loads(out.stdout.strip().splitlines()[-1]) == expect, env_val

@@ -99,22 +99,26 @@ rng = np.random.default_rng(5)
 x = [rng.integers(-1000, 1000, count).astype(np.float32) for _ in range(n)]
 exp = x[0] + x[1] + x[2]
 send = [torch.from_numpy(v).cuda() for v in x]
+waits = set()
 for proto in (ring.PROTO_SIMPLE, ring.PROTO_LL, ring.PROTO_LL128):
     with ring.RingComm(n, ring.DEVICE_MEMORY, 0, protocol=proto) as comm:
+        waits.add(comm.step_wait())
         for call in (comm.all_reduce, comm.tree_all_reduce, comm.all_reduce):
             recv = [torch.zeros_like(t) for t in send]
             torch.cuda.synchronize()
             call([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, 7, 0)
             ok = ok and all(np.array_equal(r.cpu().numpy(), exp) for r in recv)
-print(json.dumps({{"ok": bool(ok)}}))
+print(json.dumps({{"ok": bool(ok), "waits": sorted(waits), "n_vis": torch.cuda.device_count()}}))
 """
 
 
-@pytest.mark.parametrize("wait", ["sync", "word"])
+@pytest.mark.parametrize("wait", ["sync", "word", "default"])
 def test_step_wait_modes_give_the_same_results(wait):
-    """NEXR_STEP_WAIT (read once per process): the completion-word wait (default) and the plain
+    """NEXR_STEP_WAIT (read once per process): the completion-word wait and the plain
     hipStreamSynchronize wait run the ring, tree and ring all-reduces again with every protocol on one
-    communicator, in a fresh process each, and every rank of every call holds the exact sums."""
+    communicator, in a fresh process each, and every rank of every call holds the exact sums. Unset, the
+    communicator picks the word when its 3 ranks share one GPU and the synchronisation when they span
+    GPUs (rank r on GPU r mod visible); nexrRingCommGetStepWait reports the choice."""
     import json
     import os
     import subprocess
@@ -122,6 +126,11 @@ def test_step_wait_modes_give_the_same_results(wait):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = _STEP_WAIT_SCRIPT.format(root=root)
     env = dict(os.environ, NEXR_STEP_WAIT=wait)
+    if wait == "default":
+        env.pop("NEXR_STEP_WAIT")
     out = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=150)
     assert out.returncode == 0, out.stderr[-2000:]
-    assert json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])["ok"]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["ok"]
+    expect = wait if wait != "default" else ("word" if d["n_vis"] == 1 else "sync")
+    assert d["waits"] == [expect], d
