@@ -217,7 +217,8 @@ class DeviceWorkload:
         launch on the launch stream; the average kernel time of each set and where its buffers sit
         (the same kernel ran one set of C3 at 0.81-0.83 of peak and the other two at
         0.75-0.77). Each launch is followed by the same bytes as a uint32 sum (the cheapest fold,
-        v_add_u32, at that datatype's own geometry) on the same buffers: the rate this placement gives
+        v_add_u32, at the uint32 kernel's own geometry: the configuration's, except that the 16-bit K = 8
+        kernels run 1 x 1024 lanes and the uint32 one 4 x 256) on the same buffers: the rate this placement gives
         the same K + M streams, so `kernel_over_u32_sum` says what the configuration's arithmetic
         costs over the bare streams."""
         import torch
