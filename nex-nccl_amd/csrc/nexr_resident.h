@@ -1,6 +1,6 @@
 // nexr_resident.h — the device-resident ring collectives (nexr_resident.hip), shared with its host
-// side in nexr_ring.cpp. Not installed; not part of the ABI (include/nexr_ring.h declares the entry
-// point, nexrRingAllReduceResident).
+// side in nexr_resident_host.cpp. Part of the opt-in extras library (libnexr_extras.so); not installed,
+// not part of the ABI (include/nexr_extras.h declares the entry points, nexr*Resident).
 #pragma once
 #include <stdint.h>
 #include <hip/hip_runtime.h>

@@ -1,5 +1,5 @@
 // nexr_resident.hip — the ring and tree collectives as ONE device-resident launch per GPU
-// (SURVEY §8(f) #1/#4).
+// (beyond SURVEY §8: the opt-in extras library, libnexr_extras.so).
 //
 // What it runs is the reference's device kernel for ncclAllReduce with NCCL_ALGO_RING /
 // NCCL_PROTO_SIMPLE — runRing (src/device/all_reduce.h:12-84), and likewise ReduceScatter
@@ -9,7 +9,7 @@
 // waitPeer / postPeer (:111-188): NCCL_STEPS = 8 slots of stepBytes per connection, a slice spans StepPerSlice steps, the
 // receiver waits for tail >= step + StepPerSlice, the sender for head + NCCL_STEPS >= step +
 // StepPerSlice, and each side posts its step once the slice is done. The host-sequenced ring in
-// nexr_ring.cpp runs the same schedule with one reduce-copy launch per slice; this file runs every
+// nexr_ring.cpp (the default product) runs the same schedule with one reduce-copy launch per slice; this file runs every
 // rank's whole schedule inside one launch, each rank's blocks waiting on the step counters in HBM
 // instead of the host waiting on streams.
 //
