@@ -292,3 +292,33 @@ def test_multi_device_c5_full_size_work_per_gpu(nexr, dev):
     for d, (a, b, o) in enumerate(bufs):
         with torch.cuda.device(d):
             assert torch.equal(o.view(torch.int32), (a + b).view(torch.int32)), f"GPU {d}"
+
+
+def test_multi_device_c5_eight_chunks_folded_onto_one_call(nexr, dev):
+    """C5's shape from one host call whatever the box: eight full 256 MiB C2 works (fp32 sum, K=2,
+    M=1), work i on GPU i mod n. On the one-GPU box all eight threads share device 0, so the fan-out,
+    its start barrier and eight concurrent one-shot grids on one device run at the node's work size
+    (6 GiB of buffers); each output is checked bit-exactly (fp32 a+b is one IEEE add)."""
+    n = 64 << 20
+    n_dev = torch.cuda.device_count()
+    works, devices, bufs = [], [], []
+    for w in range(8):
+        d = w % n_dev
+        with torch.cuda.device(d):
+            g = torch.Generator(device=f"cuda:{d}")
+            g.manual_seed(700 + w)
+            a = torch.rand(n, device=f"cuda:{d}", generator=g) * 2 - 1
+            b = torch.rand(n, device=f"cuda:{d}", generator=g) * 2 - 1
+            o = torch.full_like(a, float("nan"))
+            bufs.append((a, b, o, d))
+            works.append(nexr.make_work([a.data_ptr(), b.data_ptr()], [o.data_ptr()], n))
+            devices.append(d)
+    for d in range(n_dev):
+        torch.cuda.synchronize(d)
+    secs = nexr.reduce_copy_multi_device(works, devices, mg.F32, 0, reps=2)
+    assert secs > 0
+    for w, (a, b, o, d) in enumerate(bufs):
+        with torch.cuda.device(d):
+            assert torch.equal(o.view(torch.int32), (a + b).view(torch.int32)), f"work {w} on GPU {d}"
+    del bufs
+    torch.cuda.empty_cache()
