@@ -182,6 +182,17 @@ def timed_steps(step, steps: int, warmup: int, sync, dist, device=None):
 
 
 # ---- one configuration on one GPU --------------------------------------------------------------
+def comparator_sequence(ns: int, rounds: int, order: str) -> list:
+    """The per-set comparator's launches as (0 = the configuration's kernel | 1 = the uint32 sum, set):
+    "grouped" runs the kernel on every set, then the uint32 sum on every set, so with two or more sets
+    no launch follows one on the same buffers; "paired" runs both back to back on each set."""
+    if order == "paired":
+        return [(kd, i % ns) for i in range(rounds * ns) for kd in (0, 1)]
+    if order == "grouped":
+        return [(kd, j) for _ in range(rounds) for kd in (0, 1) for j in range(ns)]
+    raise ValueError(f"order {order!r}")
+
+
 class DeviceWorkload:
     """R rotating buffer sets of one configuration on one GPU, and the timed launch loop over them."""
 
@@ -211,16 +222,19 @@ class DeviceWorkload:
         sp, dp, _, _ = self.sets[i % len(self.sets)]
         return self.pkg.make_work(sp, dp, self.n, self.cfg["arg"])
 
-    def per_set(self, rounds: int = 12) -> dict:
-        """After the timed region (and after check_exact: it overwrites the outputs): `rounds` x sets
-        more launches, round-robin over the sets as in the timed loop, with HIP events around every
-        launch on the launch stream; the average kernel time of each set and where its buffers sit
-        (the same kernel ran one set of C3 at 0.81-0.83 of peak and the other two at
-        0.75-0.77). Each launch is followed by the same bytes as a uint32 sum (the cheapest fold,
-        v_add_u32, at the uint32 kernel's own geometry: the configuration's, except that the 16-bit K = 8
-        kernels run 1 x 1024 lanes and the uint32 one 4 x 256) on the same buffers: the rate this placement gives
-        the same K + M streams, so `kernel_over_u32_sum` says what the configuration's arithmetic
-        costs over the bare streams."""
+    def per_set(self, rounds: int = 12, order: str = "grouped") -> dict:
+        """After the timed region (and after check_exact: it overwrites the outputs): `rounds` launches
+        per set, with HIP events around every launch on the launch stream; the average kernel time of
+        each set and where its buffers sit (the same kernel ran one set of C3 at 0.81-0.83
+        of peak and the other two at 0.75-0.77). Beside them, the same bytes as a uint32 sum (the
+        cheapest fold, v_add_u32, at the uint32 kernel's own geometry: the configuration's, except that
+        the 16-bit K = 8 kernels run 1 x 1024 lanes and the uint32 one 4 x 256) on the same buffers: the
+        rate this placement gives the same K + M streams, so `kernel_over_u32_sum` says what the
+        configuration's arithmetic costs over the bare streams. `order` (comparator_sequence):
+        "grouped", the default since round 4, never launches on the buffers the previous launch used;
+        "paired" ran the uint32 sum right after the kernel on the same set. The two give the same ratios
+        within +-0.6 % on every configuration (profiles/r04f_u32_order_ab.txt): the nt loads leave no
+        usable bytes of a set in the Infinity Cache."""
         import torch
         cfg, ns = self.cfg, len(self.sets)
         n32 = cfg["buf_bytes"] // 4
@@ -231,14 +245,15 @@ class DeviceWorkload:
             sp, dp, _, _ = self.sets[-1]
             self.pkg.reduce_copy_ptrs(sp, dp, self.n, cfg["dt"], cfg["op"], cfg["arg"], None, False, self.handle)
             self.pkg.reduce_copy_ptrs(sp, dp, n32, 3, 0, 0, None, False, self.handle)
-            for i in range(rounds * ns):
-                sp, dp, _, _ = self.sets[i % ns]
-                for kind, n, dt, op, arg in (("kernel", self.n, cfg["dt"], cfg["op"], cfg["arg"]), ("u32", n32, 3, 0, 0)):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(self.stream)
-                    self.pkg.reduce_copy_ptrs(sp, dp, n, dt, op, arg, None, False, self.handle)
-                    e1.record(self.stream)
-                    evs.append((kind, i % ns, e0, e1))
+            kinds = (("kernel", self.n, cfg["dt"], cfg["op"], cfg["arg"]), ("u32", n32, 3, 0, 0))
+            for kd, j in comparator_sequence(ns, rounds, order):
+                kind, n, dt, op, arg = kinds[kd]
+                sp, dp, _, _ = self.sets[j]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
+                self.pkg.reduce_copy_ptrs(sp, dp, n, dt, op, arg, None, False, self.handle)
+                e1.record(self.stream)
+                evs.append((kind, j, e0, e1))
             torch.cuda.synchronize(self.dev)
         us = {"kernel": [[] for _ in range(ns)], "u32": [[] for _ in range(ns)]}
         for kind, k, e0, e1 in evs:
@@ -248,7 +263,7 @@ class DeviceWorkload:
         lo = min(p for sp, dp, _, _ in self.sets for p in sp + dp)
         return {"per_set_us": [round(x, 2) for x in ker],
                 "per_set_frac": [round(algorithmic_bytes(cfg) / x / 1e3 / PEAK_HBM_GBS, 4) for x in ker],
-                "per_set_launches": rounds,
+                "per_set_launches": rounds, "per_set_order": order,
                 "per_set_buffers_mib": [[round((p - lo) / (1 << 20), 3) for p in sp + dp] for sp, dp, _, _ in self.sets],
                 "same_bytes_u32_sum_per_set_us": [round(x, 2) for x in u32],
                 "kernel_over_u32_sum": round(mean(ker) / mean(u32), 4)}

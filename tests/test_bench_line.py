@@ -404,3 +404,17 @@ def test_xgmi_probe_skipped_on_one_gpu(monkeypatch):
     monkeypatch.setattr(bench, "_bounded", lambda cmd, t: calls.append(cmd) or {})
     res = bench.xgmi_probe()
     assert "skipped" in res and calls == []
+
+
+def test_comparator_sequence_orders():
+    """The per-set comparator (DeviceWorkload.per_set): both orders launch the kernel and the uint32 sum
+    `rounds` times on every set; "grouped" never launches on the set the previous launch used (so
+    neither side finds the other's bytes in the Infinity Cache), "paired" does so by construction."""
+    for ns in (2, 3, 4):
+        for order in ("grouped", "paired"):
+            seq = bench.comparator_sequence(ns, 5, order)
+            assert sorted(seq) == sorted((kd, j) for kd in (0, 1) for j in range(ns) for _ in range(5))
+            same = sum(a[1] == b[1] for a, b in zip(seq, seq[1:]))
+            assert (same == 0) if order == "grouped" else (same == 5 * ns)
+    with pytest.raises(ValueError):
+        bench.comparator_sequence(3, 1, "other")
