@@ -1,0 +1,132 @@
+"""nexrReduceCopyHost on host memory the caller registered with hipHostRegister (include/nexr.h: "when
+every buffer is pinned host memory (hipHostMalloc / hipHostRegister / torch pin_memory) the kernel
+reads and writes it in place"). The fork's transport allocates its staging buffers once
+(src/include/device.h:753-771), so registering them once is how a caller gets the zero-copy path on
+memory it did not allocate with the HIP runtime.
+
+Every pointer here lies INSIDE one registered mapping, at offsets that are not page-aligned, so the
+library's device address for each must be the mapping's device base plus the offset; a wrong
+translation would read or write the wrong bytes and the exact check would fail. fp32 a + b is one
+IEEE add, so numpy's float32 sum is the oracle's value bit for bit."""
+import ctypes
+import importlib
+import mmap
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HIP_HOST_REGISTER_MAPPED = 2  # hipHostRegisterMapped
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    torch.cuda.init()
+    L = ctypes.CDLL("libamdhip64.so")
+    L.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    L.hipHostRegister.restype = ctypes.c_int
+    L.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    L.hipHostUnregister.restype = ctypes.c_int
+    return L
+
+
+class Region:
+    """One anonymous mapping (page-aligned), registered with hipHostRegister for its lifetime."""
+
+    def __init__(self, hip, nbytes: int, register: bool = True):
+        self.hip, self.m = hip, mmap.mmap(-1, nbytes)
+        self.buf = np.frombuffer(self.m, dtype=np.uint8)
+        self.base = self.buf.ctypes.data
+        self.registered = False
+        if register:
+            rc = hip.hipHostRegister(self.base, nbytes, HIP_HOST_REGISTER_MAPPED)
+            assert rc == 0, f"hipHostRegister = {rc}"
+            self.registered = True
+
+    def f32(self, offset: int, n: int) -> np.ndarray:
+        return self.buf[offset:offset + 4 * n].view(np.float32)
+
+    def close(self):
+        """Unregisters; the mapping itself goes when the last numpy view of it does."""
+        if self.registered:
+            self.registered = False
+            assert self.hip.hipHostUnregister(self.base) == 0
+
+
+def _fill(rng, v: np.ndarray):
+    v[:] = rng.random(v.size, dtype=np.float32) * 2 - 1
+
+
+@pytest.mark.parametrize("n", [1, 4099, 1_000_003, 16 << 20])
+def test_registered_interior_pointers_zero_copy(hip, n):
+    nexr = importlib.import_module("nex-nccl_amd")
+    rng = np.random.default_rng(n)
+    gap = 4096 * 3 + 48  # offsets inside the mapping that are not page- (or even 64 B-) aligned
+    offs = [gap + 16, 2 * gap + 4 * n + 4, 3 * gap + 8 * n + 12]
+    reg = Region(hip, offs[-1] + 4 * n + gap)
+    try:
+        a, b, out = (reg.f32(o, n) for o in offs)
+        _fill(rng, a)
+        _fill(rng, b)
+        out[:] = np.nan
+        guard_before = reg.buf[offs[2] - 64:offs[2]].copy()
+        guard_after = reg.buf[offs[2] + 4 * n:offs[2] + 4 * n + 64].copy()
+        nexr.reduce_copy_ptrs([reg.base + offs[0], reg.base + offs[1]], [reg.base + offs[2]], n, 7, 0, host=True)
+        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+        assert np.array_equal(reg.buf[offs[2] - 64:offs[2]], guard_before)
+        assert np.array_equal(reg.buf[offs[2] + 4 * n:offs[2] + 4 * n + 64], guard_after)
+    finally:
+        reg.close()
+
+
+def test_registered_sources_pageable_destination(hip):
+    """A mix: the sources in a registered mapping, the destination in plain pageable memory (the
+    library reads the registered ones in place and stages only the destination)."""
+    nexr = importlib.import_module("nex-nccl_amd")
+    n = 3_000_017
+    rng = np.random.default_rng(7)
+    reg = Region(hip, 8 * n + 8192)
+    try:
+        a, b = reg.f32(4096 + 4, n), reg.f32(4096 + 4 + 4 * n, n)
+        _fill(rng, a)
+        _fill(rng, b)
+        out = np.full(n, np.nan, dtype=np.float32)
+        nexr.reduce_copy_ptrs([a.ctypes.data, b.ctypes.data], [out.ctypes.data], n, 7, 0, host=True)
+        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+    finally:
+        reg.close()
+
+
+def test_registered_rate_beside_pageable(hip):
+    """C2's mix (2 x 256 MiB in, 1 out) on one registered mapping against the same bytes unregistered:
+    both exact; the registered call takes the zero-copy path, so it is not slower than the pageable
+    one (both rates printed; the bench's h2d_inclusive line carries the measured figures)."""
+    nexr = importlib.import_module("nex-nccl_amd")
+    n = 64 << 20
+    rng = np.random.default_rng(11)
+    secs = {}
+    for register in (True, False):
+        reg = Region(hip, 12 * n + 3 * 4096, register=register)
+        try:
+            a, b, out = reg.f32(0, n), reg.f32(4 * n + 4096, n), reg.f32(8 * n + 8192, n)
+            _fill(rng, a)
+            _fill(rng, b)
+            ptrs = ([reg.base, reg.base + 4 * n + 4096], [reg.base + 8 * n + 8192])
+            nexr.reduce_copy_ptrs(*ptrs, n, 7, 0, host=True)  # warm-up (staging rings, code objects)
+            t = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                nexr.reduce_copy_ptrs(*ptrs, n, 7, 0, host=True)
+                t.append(time.perf_counter() - t0)
+            assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+            secs[register] = min(t)
+        finally:
+            reg.close()
+    gbs = {k: 12 * n / v / 1e9 for k, v in secs.items()}
+    print(f"registered {gbs[True]:.1f} GB/s, pageable {gbs[False]:.1f} GB/s")
+    assert secs[True] <= secs[False] * 1.10, gbs
