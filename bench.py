@@ -399,7 +399,9 @@ def c1_ring(iters: int = 20) -> dict:
             ("device_ll", ring.DEVICE_MEMORY, None, ring.PROTO_LL),
             ("device_ll128", ring.DEVICE_MEMORY, None, ring.PROTO_LL128),
             ("host_staged", ring.HOST_MEMORY, None, ring.PROTO_SIMPLE),
+            ("host_registered", ring.HOST_MEMORY, None, ring.PROTO_SIMPLE),
             ("cpu_oracle", ring.HOST_MEMORY, cpu_fn, ring.PROTO_SIMPLE))
+    nexr = importlib.import_module("nex-nccl_amd")
     for name, mode, fn, proto in legs:
         if mode == ring.DEVICE_MEMORY:  # rank r's buffers on rank r's GPU (libnexr_ring: r mod visible)
             devs = [torch.device("cuda", r % torch.cuda.device_count()) for r in range(n)]
@@ -413,16 +415,34 @@ def c1_ring(iters: int = 20) -> dict:
         sp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in send]
         rp = [t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data for t in recv]
         reps = iters if fn is None else max(2, iters // 10)
-        with ring.RingComm(n, mode, 0, fn, protocol=proto, timeout_ms=10000) as comm:
-            wait = comm.step_wait()
-            comm.all_reduce(sp, rp, count, 7, 0)
-            t0 = time.perf_counter()
-            for _ in range(reps):
+        # host_registered: the integration INTEGRATION.md §2b recommends — the user buffers registered
+        # once with nexrHostRegister (outside the timing), so every step is one zero-copy kernel whose
+        # buffers are classified from the registration cache (the FIFOs come from nexrHostMemAlloc)
+        handles = [nexr.host_register(a.ctypes.data, a.nbytes) for a in send + recv] if name == "host_registered" else []
+        try:
+            with ring.RingComm(n, mode, 0, fn, protocol=proto, timeout_ms=10000) as comm:
+                wait = comm.step_wait()
                 comm.all_reduce(sp, rp, count, 7, 0)
-            dt = (time.perf_counter() - t0) / reps
+                nexr.host_path_stats(reset=True)
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    comm.all_reduce(sp, rp, count, 7, 0)
+                dt = (time.perf_counter() - t0) / reps
+                hp = nexr.host_path_stats(reset=True)
+        finally:
+            for h in handles:
+                nexr.host_deregister(h)
         got = [r.cpu().numpy() if hasattr(r, "cpu") else r for r in recv]
         out[name] = {"ms_per_call": round(dt * 1e3, 3), "algbw_gbs": round(count * 4 / dt / 1e9, 2), "calls": reps,
                      "exact": all(np.array_equal(g, expect) for g in got)}
+        if mode == ring.HOST_MEMORY and fn is None and hp["calls"]:
+            # per reduce-copy step (nexrGetHostPathStats, summed over both rank threads): where the
+            # host time of nexrReduceCopyHost goes; wait includes the kernel's run over PCIe
+            steps = hp["calls"]
+            out[name]["per_step"] = {
+                "steps_per_call": round(steps / reps, 2), "zero_copy_steps": hp["zeroCopyCalls"] / steps,
+                "registered_hits": hp["registeredHits"], "pointer_queries": hp["pointerQueries"],
+                **{f"{k}_us": round(hp[k + "Ns"] / steps / 1e3, 2) for k in ("classify", "copy", "launch", "wait")}}
         if mode == ring.DEVICE_MEMORY:
             out[name]["step_wait"] = wait  # "word" with both ranks on one GPU, "sync" across GPUs
     out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_ll / device_ll128 run the same ring "

@@ -201,6 +201,44 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
                                          nexrStream_t stream);
 
 /*
+ * Host-memory registration — replaces ncclCommRegister / ncclCommDeregister (reference
+ * src/nccl.h.in:243-246, src/register/register.cc:128-170) and ncclMemAlloc / ncclMemFree
+ * (src/nccl.h.in:130-133, src/allocator.cc) for the fork's setting, where NEX "device memory" and
+ * the transport's staging FIFOs are host memory.
+ *   nexrHostRegister    page-locks and device-maps [buff, buff + size) (hipHostRegister, mapped +
+ *                       portable) and records it in a process-wide cache sorted by address, like
+ *                       the reference's regCache (register.cc:40-60). A range inside one already
+ *                       registered here shares that entry (reference count); a range that partly
+ *                       overlaps one returns nexrInvalidUsage. *handle identifies the entry.
+ *   nexrHostDeregister  drops one reference; the last one unregisters the range (NULL: no-op).
+ *   nexrHostMemAlloc    pinned, device-mapped host memory (hipHostMalloc), recorded in the same cache.
+ *   nexrHostMemFree     frees memory from nexrHostMemAlloc (NULL: no-op).
+ * nexrReduceCopyHost looks every buffer up in this cache first: a buffer wholly inside an entry is
+ * read and written in place over PCIe with no runtime query. Other pinned memory (registered by the
+ * caller directly) is still found with hipPointerGetAttributes on every call. Do not free or
+ * unregister a range behind the library's back while it is registered here.
+ */
+NEXR_API nexrResult_t nexrHostRegister(void* buff, size_t size, void** handle);
+NEXR_API nexrResult_t nexrHostDeregister(void* handle);
+NEXR_API nexrResult_t nexrHostMemAlloc(void** ptr, size_t size);
+NEXR_API nexrResult_t nexrHostMemFree(void* ptr);
+
+/*
+ * nexrGetHostPathStats — diagnostics: where nexrReduceCopyHost calls have spent host time since the
+ * last reset (process-wide, every thread). calls / zeroCopyCalls: calls, and those whose every buffer
+ * was pinned (one kernel over PCIe, no copies); registeredHits / pointerQueries: buffers classified
+ * from the registration cache / by a runtime pointer query; classifyNs: classifying the buffers;
+ * copyNs: host staging copies; launchNs: queuing kernels (and, on the runtime-copy pipeline, its
+ * asynchronous copies); waitNs: waiting for the stream or a slot's kernel (kernel run time included).
+ * reset != 0 zeroes the counters after reading them.
+ */
+typedef struct {
+  uint64_t calls, zeroCopyCalls, registeredHits, pointerQueries;
+  uint64_t classifyNs, copyNs, launchNs, waitNs;
+} nexrHostPathStats;
+NEXR_API nexrResult_t nexrGetHostPathStats(nexrHostPathStats* stats, int reset);
+
+/*
  * nexrHostToDevRedOp — replaces hostToDevRedOp (reference src/enqueue.cc:2185-2278) for the
  * built-in ops: encodes (op, datatype, nRanks) into the device op and its 64-bit argument
  * (Min/Max xormask, Avg: integer nRanks<<1|signed or float 1/nRanks bit pattern).

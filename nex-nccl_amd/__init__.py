@@ -86,7 +86,8 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
 ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyMultiDeviceSets",
                "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
                "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrQueryLaunch", "nexrGetPoolStats", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion",
-               "nexrGetLastHipError", "nexrSetSemantics", "nexrGetSemantics")
+               "nexrGetLastHipError", "nexrSetSemantics", "nexrGetSemantics", "nexrHostRegister", "nexrHostDeregister",
+               "nexrHostMemAlloc", "nexrHostMemFree", "nexrGetHostPathStats")
 
 
 class NexrError(RuntimeError):
@@ -112,6 +113,12 @@ class LaunchInfo(ctypes.Structure):
                 ("policy", ctypes.c_int), ("generic", ctypes.c_int), ("unaligned", ctypes.c_int),
                 ("headElts", ctypes.c_uint64),
                 ("bodyPacks", ctypes.c_uint64)]
+
+
+class HostPathStats(ctypes.Structure):
+    """Mirror of nexrHostPathStats (include/nexr.h): nexrGetHostPathStats' counters."""
+    _fields_ = [(f, ctypes.c_uint64) for f in ("calls", "zeroCopyCalls", "registeredHits", "pointerQueries",
+                                               "classifyNs", "copyNs", "launchNs", "waitNs")]
 
 
 MAX_BATCH_WORKS = 14  # NEXR_MAX_BATCH_WORKS
@@ -212,6 +219,16 @@ def lib() -> ctypes.CDLL:
     L.nexrGetVersion.restype = i32
     L.nexrGetLastHipError.argtypes = []
     L.nexrGetLastHipError.restype = i32
+    L.nexrHostRegister.argtypes = [vp, sz, P(vp)]
+    L.nexrHostRegister.restype = i32
+    L.nexrHostDeregister.argtypes = [vp]
+    L.nexrHostDeregister.restype = i32
+    L.nexrHostMemAlloc.argtypes = [P(vp), sz]
+    L.nexrHostMemAlloc.restype = i32
+    L.nexrHostMemFree.argtypes = [vp]
+    L.nexrHostMemFree.restype = i32
+    L.nexrGetHostPathStats.argtypes = [P(HostPathStats), i32]
+    L.nexrGetHostPathStats.restype = i32
     _lib = L
     return L
 
@@ -332,6 +349,38 @@ def pool_stats() -> tuple:
     a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
     _check(lib().nexrGetPoolStats(ctypes.byref(a), ctypes.byref(b)), "nexrGetPoolStats")
     return a.value, b.value
+
+
+def host_register(addr: int, nbytes: int) -> int:
+    """nexrHostRegister (ncclCommRegister's counterpart for host memory): page-lock and device-map
+    [addr, addr + nbytes) and record it in libnexr's registration cache. Returns the handle."""
+    h = ctypes.c_void_p()
+    _check(lib().nexrHostRegister(ctypes.c_void_p(int(addr)), int(nbytes), ctypes.byref(h)), "nexrHostRegister")
+    return int(h.value or 0)
+
+
+def host_deregister(handle: int) -> None:
+    """nexrHostDeregister: drop one reference to a registration (the last one unregisters)."""
+    _check(lib().nexrHostDeregister(ctypes.c_void_p(int(handle)) if handle else None), "nexrHostDeregister")
+
+
+def host_mem_alloc(nbytes: int) -> int:
+    """nexrHostMemAlloc (ncclMemAlloc's counterpart): pinned, device-mapped host memory."""
+    p = ctypes.c_void_p()
+    _check(lib().nexrHostMemAlloc(ctypes.byref(p), int(nbytes)), "nexrHostMemAlloc")
+    return int(p.value)
+
+
+def host_mem_free(addr: int) -> None:
+    _check(lib().nexrHostMemFree(ctypes.c_void_p(int(addr)) if addr else None), "nexrHostMemFree")
+
+
+def host_path_stats(reset: bool = False) -> dict:
+    """nexrGetHostPathStats: where nexrReduceCopyHost calls have spent host time (ns) since the last
+    reset, with the counts of calls, zero-copy calls, cache hits and runtime pointer queries."""
+    st = HostPathStats()
+    _check(lib().nexrGetHostPathStats(ctypes.byref(st), 1 if reset else 0), "nexrGetHostPathStats")
+    return {f: int(getattr(st, f)) for f, _ in HostPathStats._fields_}
 
 
 def set_semantics(mode: int) -> None:

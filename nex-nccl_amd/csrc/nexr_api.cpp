@@ -10,6 +10,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -29,6 +30,16 @@ inline nexrResult_t hipFail(hipError_t e) {
     hipError_t e_ = (call);                     \
     if (e_ != hipSuccess) return hipFail(e_);   \
   } while (0)
+
+// ---- host-path counters (nexrGetHostPathStats): where a nexrReduceCopyHost call spends its time
+std::atomic<uint64_t> gHpCalls{0}, gHpZeroCopy{0}, gHpRegHits{0}, gHpQueries{0};
+std::atomic<uint64_t> gHpClassifyNs{0}, gHpCopyNs{0}, gHpLaunchNs{0}, gHpWaitNs{0};
+inline uint64_t nowNs() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 
 size_t typeSize(int dt) {
   switch (dt) {
@@ -273,7 +284,11 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
     op = c0.op;
   }
   const size_t esz = typeSize(datatype);
-  for (int k = 1; k <= NEXR_MAX_SRCS; k++) {
+  // One run per (K, and for MinMax isMin = (redOpArg & 1) == 0): the kernel is compiled per isMin.
+  const int nMin = op == nexrDevMinMax ? 2 : 1;
+  for (int kk = 0; kk < NEXR_MAX_SRCS * nMin; kk++) {
+    const int k = 1 + kk / nMin;
+    const int minClass = kk % nMin;  // MinMax: 0 = max (arg bit 0 set), 1 = min
     BatchParams b;
     b.nWorks = 0;
     uint64_t blocks[kMaxBatch];
@@ -313,6 +328,7 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
     for (int i = 0; i < nWorks; i++) {
       const nexrReduceCopyWork& w = works[i];
       if (w.nSrcs != k || w.nElts == 0 || w.nDsts == 0) continue;
+      if (nMin == 2 && (int)((w.redOpArg & 1) == 0) != minClass) continue;
       RCParams& p = b.w[b.nWorks];
       fillParams(p, k, w.srcs, w.nDsts, w.dsts, w.nElts, esz, w.redOpArg, w.nPreOpSrcs, w.preOpArgs, nullptr,
                  w.postOp);
@@ -796,15 +812,22 @@ nexrResult_t reduceCopyHostTeam(int nSrcs, const void* const* srcs, const bool* 
   // reduces chunk c-1; then chunk c's kernel is queued.
   for (size_t c = 0; c < nChunks + 2; c++) {
     nTasks = 0;
+    uint64_t t0 = nowNs();
     if (c >= 2) {
       NEXR_HIP(hipEventSynchronize(st->done[(c - 2) % kPinnedSlots]));
+      const uint64_t t1 = nowNs();
+      gHpWaitNs.fetch_add(t1 - t0, std::memory_order_relaxed);
+      t0 = t1;
       if (outStaged) copyOut(c - 2);
     }
     if (c < nChunks) copyIn(c);
     if (nTasks > 0) team.run(tasks, nTasks);
+    const uint64_t t1 = nowNs();
+    gHpCopyNs.fetch_add(t1 - t0, std::memory_order_relaxed);
     if (c < nChunks) {
       r = launch(c);
       if (r != nexrSuccess) return r;
+      gHpLaunchNs.fetch_add(nowNs() - t1, std::memory_order_relaxed);
     }
   }
   return nexrSuccess;
@@ -839,6 +862,49 @@ uint16_t floatToBf16Rne(float f) {
   memcpy(&u, &f, 4);
   if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fffu;
   return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+// ---- host registration cache (reference: ncclCommRegister's per-comm regCache, sorted by begin
+// address, src/register/register.cc:40-60; ncclMemAlloc, src/allocator.cc:11-) -----------------
+// Pinned, device-mapped host ranges the library registered (nexrHostRegister) or allocated
+// (nexrHostMemAlloc), sorted by begin address. nexrReduceCopyHost looks a buffer up here first, so a
+// call on registered memory costs no HIP query per buffer; because the library made every entry, it
+// also knows when one ends (nexrHostDeregister / nexrHostMemFree), so nothing here goes stale.
+struct HostReg {
+  uintptr_t beg = 0, end = 0;
+  char* dev = nullptr;  // device address of beg
+  bool owned = false;   // allocated by nexrHostMemAlloc (freed by nexrHostMemFree), else registered
+  int refs = 1;
+};
+std::shared_mutex gRegMu;
+std::vector<HostReg*> gRegs;  // sorted by beg, non-overlapping
+
+// The device address of [p, p + bytes) when the whole range lies inside one entry.
+bool regLookup(const void* p, size_t bytes, void** dev) {
+  const uintptr_t a = (uintptr_t)p;
+  std::shared_lock<std::shared_mutex> lk(gRegMu);
+  auto it = std::upper_bound(gRegs.begin(), gRegs.end(), a, [](uintptr_t v, const HostReg* r) { return v < r->beg; });
+  if (it == gRegs.begin()) return false;
+  const HostReg* r = *(it - 1);
+  if (a + bytes > r->end || a + bytes < a) return false;
+  *dev = r->dev + (a - r->beg);
+  return true;
+}
+
+// Index of the entry containing [a, a + n), -1 if none; overlap: some entry intersects it.
+int regFind(uintptr_t a, size_t n, bool* overlap) {
+  *overlap = false;
+  for (size_t i = 0; i < gRegs.size(); i++) {
+    const HostReg* r = gRegs[i];
+    if (a >= r->beg && a + n <= r->end) return (int)i;
+    if (a < r->end && a + n > r->beg) *overlap = true;
+  }
+  return -1;
+}
+
+void regInsert(HostReg* r) {
+  auto it = std::upper_bound(gRegs.begin(), gRegs.end(), r->beg, [](uintptr_t v, const HostReg* x) { return v < x->beg; });
+  gRegs.insert(it, r);
 }
 
 }  // namespace
@@ -930,31 +996,62 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
   const void* zsrc[NEXR_MAX_SRCS];
   void* zdst[NEXR_MAX_DSTS];
   bool psrc[NEXR_MAX_SRCS], pdst[NEXR_MAX_DSTS];  // pinned (device-mapped) buffers
+  // Classification: the registration cache first (no HIP call); otherwise the runtime's pointer
+  // query, trusted only when the whole buffer lies inside the pinned range it reports.
   static const long zeroCopy = envLong("NEXR_HOST_ZERO_COPY", 1);
+  const size_t esz = typeSize(datatype);
+  const size_t bufBytes = nElts * esz;
+  const uint64_t tc0 = nowNs();
+  gHpCalls.fetch_add(1, std::memory_order_relaxed);
   int nPinned = 0;
   for (int k = 0; k < nSrcs + nDsts; k++) {
     const void* hp = k < nSrcs ? srcs[k] : dsts[k - nSrcs];
-    hipPointerAttribute_t a;
-    bool pin = zeroCopy != 0 && hipPointerGetAttributes(&a, hp) == hipSuccess && a.type == hipMemoryTypeHost &&
-               a.devicePointer != nullptr;
-    if (!pin) (void)hipGetLastError();  // pageable memory reports an error: not a failure of this call
+    void* dev = nullptr;
+    bool pin = false;
+    if (zeroCopy != 0) {
+      if (regLookup(hp, bufBytes, &dev)) {
+        pin = true;
+        gHpRegHits.fetch_add(1, std::memory_order_relaxed);
+      } else {
+        gHpQueries.fetch_add(1, std::memory_order_relaxed);
+        hipPointerAttribute_t a;
+        pin = hipPointerGetAttributes(&a, hp) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer != nullptr;
+        if (pin) {
+          dev = a.devicePointer;
+          // A pointer inside a registered range whose buffer runs past its end must not be read in
+          // place: the device mapping covers only the range. Without the range, nothing is.
+          uintptr_t beg = 0;
+          size_t size = 0;
+          if (hipPointerGetAttribute(&beg, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)hp) != hipSuccess ||
+              hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)hp) != hipSuccess ||
+              (uintptr_t)hp < beg || (uintptr_t)hp + bufBytes > beg + size)
+            pin = false;
+        }
+        (void)hipGetLastError();  // pageable memory reports an error: not a failure of this call
+      }
+    }
     if (k < nSrcs) {
       psrc[k] = pin;
-      zsrc[k] = pin ? a.devicePointer : nullptr;
+      zsrc[k] = pin ? dev : nullptr;
     } else {
       pdst[k - nSrcs] = pin;
-      zdst[k - nSrcs] = pin ? a.devicePointer : nullptr;
+      zdst[k - nSrcs] = pin ? dev : nullptr;
     }
     nPinned += pin ? 1 : 0;
   }
+  const uint64_t tc1 = nowNs();
+  gHpClassifyNs.fetch_add(tc1 - tc0, std::memory_order_relaxed);
   if (nPinned == nSrcs + nDsts) {
+    gHpZeroCopy.fetch_add(1, std::memory_order_relaxed);
     r = reduceCopyDevice(nSrcs, zsrc, nDsts, zdst, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs,
                          nullptr, postOp, s);
+    const uint64_t tc2 = nowNs();
+    gHpLaunchNs.fetch_add(tc2 - tc1, std::memory_order_relaxed);
     if (r != nexrSuccess) return r;
     NEXR_HIP(hipStreamSynchronize(s));
+    gHpWaitNs.fetch_add(nowNs() - tc2, std::memory_order_relaxed);
     return nexrSuccess;
   }
-  const size_t esz = typeSize(datatype);
   // Pageable buffers, by the pageable bytes the call moves (profiles/r02_host_sizes_sweep.log):
   //   <= NEXR_HOST_SOLO_MAX_BYTES (4 MiB; the emulated ring's slices): the calling thread copies them
   //      into pinned zero-copy slots (reduceCopyHostTeam, one thread): 1.2-1.9x the runtime copies;
@@ -983,6 +1080,7 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
   bool anyPageableDst = false;
   for (int d = 0; d < nDsts; d++) anyPageableDst |= !pdst[d];
   const size_t nChunks = (nElts + chunkElts - 1) / chunkElts;
+  const uint64_t tp = nowNs();
   for (size_t c = 0; c < nChunks; c++) {
     const int slot = (int)(c & 1);
     const size_t e0 = c * chunkElts;
@@ -1014,8 +1112,101 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
         NEXR_HIP(hipMemcpyAsync((char*)dsts[d] + e0 * esz, staged, n * esz, hipMemcpyDeviceToHost, st->out));
     NEXR_HIP(hipEventRecord(st->outDone[slot], st->out));
   }
+  const uint64_t tw = nowNs();
+  gHpLaunchNs.fetch_add(tw - tp, std::memory_order_relaxed);
   NEXR_HIP(hipStreamSynchronize(st->out));
   NEXR_HIP(hipStreamSynchronize(s));
+  gHpWaitNs.fetch_add(nowNs() - tw, std::memory_order_relaxed);
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrHostRegister(void* buff, size_t size, void** handle) {
+  if (buff == nullptr || size == 0 || handle == nullptr) return nexrInvalidArgument;
+  const uintptr_t a = (uintptr_t)buff;
+  std::unique_lock<std::shared_mutex> lk(gRegMu);
+  bool overlap = false;
+  const int i = regFind(a, size, &overlap);
+  if (i >= 0) {  // inside a range this library already registered: share it (register.cc:49-76)
+    gRegs[i]->refs++;
+    *handle = gRegs[i];
+    return nexrSuccess;
+  }
+  if (overlap) return nexrInvalidUsage;  // partly inside another entry: hipHostRegister would refuse it
+  NEXR_HIP(hipHostRegister(buff, size, hipHostRegisterMapped | hipHostRegisterPortable));
+  void* dev = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dev, buff, 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(buff);
+    return hipFail(e);
+  }
+  HostReg* r = new HostReg();
+  r->beg = a;
+  r->end = a + size;
+  r->dev = (char*)dev;
+  regInsert(r);
+  *handle = r;
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrHostDeregister(void* handle) {
+  if (handle == nullptr) return nexrSuccess;  // ncclCommDeregister accepts a NULL handle
+  std::unique_lock<std::shared_mutex> lk(gRegMu);
+  auto it = std::find(gRegs.begin(), gRegs.end(), (HostReg*)handle);
+  if (it == gRegs.end() || (*it)->owned) return nexrInvalidUsage;  // register.cc:150-153
+  HostReg* r = *it;
+  if (--r->refs > 0) return nexrSuccess;
+  gRegs.erase(it);
+  hipError_t e = hipHostUnregister((void*)r->beg);
+  delete r;
+  NEXR_HIP(e);
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrHostMemAlloc(void** ptr, size_t size) {
+  if (ptr == nullptr || size == 0) return nexrInvalidArgument;
+  *ptr = nullptr;
+  void* host = nullptr;
+  NEXR_HIP(hipHostMalloc(&host, size, hipHostMallocMapped | hipHostMallocPortable));
+  void* dev = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dev, host, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(host);
+    return hipFail(e);
+  }
+  HostReg* r = new HostReg();
+  r->beg = (uintptr_t)host;
+  r->end = (uintptr_t)host + size;
+  r->dev = (char*)dev;
+  r->owned = true;
+  std::unique_lock<std::shared_mutex> lk(gRegMu);
+  regInsert(r);
+  *ptr = host;
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrHostMemFree(void* ptr) {
+  if (ptr == nullptr) return nexrSuccess;
+  std::unique_lock<std::shared_mutex> lk(gRegMu);
+  auto it = std::find_if(gRegs.begin(), gRegs.end(), [&](const HostReg* r) { return r->owned && r->beg == (uintptr_t)ptr; });
+  if (it == gRegs.end()) return nexrInvalidArgument;
+  HostReg* r = *it;
+  gRegs.erase(it);
+  delete r;
+  NEXR_HIP(hipHostFree(ptr));
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrGetHostPathStats(nexrHostPathStats* stats, int reset) {
+  if (stats == nullptr) return nexrInvalidArgument;
+  auto take = [&](std::atomic<uint64_t>& a) { return reset ? a.exchange(0) : a.load(); };
+  stats->calls = take(gHpCalls);
+  stats->zeroCopyCalls = take(gHpZeroCopy);
+  stats->registeredHits = take(gHpRegHits);
+  stats->pointerQueries = take(gHpQueries);
+  stats->classifyNs = take(gHpClassifyNs);
+  stats->copyNs = take(gHpCopyNs);
+  stats->launchNs = take(gHpLaunchNs);
+  stats->waitNs = take(gHpWaitNs);
   return nexrSuccess;
 }
 

@@ -138,10 +138,17 @@ __host__ __device__ constexpr int unroll_for(int dt, int k, int pol) {
                                                                 : 4;
 }
 __host__ __device__ constexpr int block_for(int dt, int k, int pol) { return kTripPacks / unroll_for(dt, k, pol); }
-// Load / store order inside a trip (nexr_kernels.hip body()): source-major (every source's pack u = 0,
-// then u = 1, ...; all packs stored after the last fold). Pack-major (pack by pack, each stored after
-// its fold) was 0.5-2.6 % slower on C2, C4 and the other U > 1 geometries, byte-identical
-// (tools/pack_order_ab.hip, profiles/r04b_pack_order_ab_not_kept.txt); the switch stays for that harness.
-__host__ __device__ constexpr bool pack_major_for(int, int, int) { return false; }
+// Workgroups per CU: the registers of the round-5 kernels admit two 1024-lane workgroups of the 16-bit
+// K = 8 geometry per CU (256 KiB of loads in flight per CU); one is 1.4-3.0 % faster on four boxes,
+// for fp16 and bf16 alike (tools/body_ab.hip, tools/occupancy_ab.hip, tools/data_ab.hip;
+// profiles/r05a_body_ab.txt, r05b_occupancy_ab.txt, r05c_data_ab.txt). The launch reserves this many
+// bytes of dynamic LDS (the kernel never touches it) so that only one fits in a CU's 160 KiB. Every
+// other geometry runs as its registers allow: C2 is flat from 2 to 8 workgroups per CU, C4 from 2 to 4.
+constexpr int kLdsOneWorkgroupPerCu = 120 * 1024;
+__host__ __device__ constexpr int lds_for(int dt, int k, int pol) {
+  return unroll_for(dt, k, pol) == 1 && block_for(dt, k, pol) == 1024 && (dt == nexrFloat16 || dt == nexrBfloat16)
+             ? kLdsOneWorkgroupPerCu
+             : 0;
+}
 
 }  // namespace nexr

@@ -446,9 +446,10 @@ nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes) {
   } else if (c->needHip && pinnedHostFifos()) {
     // Host memory with the MI355X doing the steps: pinned, device-mapped FIFOs, so that a step whose
     // user buffers are pinned too runs as one zero-copy kernel over PCIe (nexrReduceCopyHost) instead
-    // of staging every slice through device memory.
-    if (hipHostMalloc((void**)&k->fifo, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
-      return nexrUnhandledCudaError;
+    // of staging every slice through device memory. nexrHostMemAlloc records the FIFO in libnexr's
+    // registration cache, so no step queries the runtime to classify it.
+    nexrResult_t r = nexrHostMemAlloc((void**)&k->fifo, bytes);
+    if (r != nexrSuccess) return r;
     k->pinned = true;
   } else {
     k->fifo = (char*)aligned_alloc(4096, bytes);
@@ -530,7 +531,7 @@ void freeConn(nexrRingComm* c, Conn* k) {
       (void)hipSetDevice(k->device);
       (void)hipFree(k->fifo);
     } else if (k->pinned) {
-      (void)hipHostFree(k->fifo);
+      (void)nexrHostMemFree(k->fifo);
     } else {
       free(k->fifo);
     }

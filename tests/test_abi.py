@@ -91,6 +91,28 @@ def test_invalid_arguments_fail_before_the_device(nexr):
     assert L.nexrReduceCopy(2, sa, 1, da, 16, 7, 0, 0, 1, None, 0, None) == 4  # preOpArgs NULL
 
 
+def test_host_registration_validates_before_the_device(nexr):
+    """nexrHostRegister / Deregister / MemAlloc / MemFree / GetHostPathStats reject bad arguments and
+    accept the NULL no-ops (ncclCommDeregister and ncclMemFree take NULL, register.cc:147, allocator.cc)
+    with no HIP call; the stats read and reset without a device."""
+    L = nexr.lib()
+    h = ctypes.c_void_p()
+    assert L.nexrHostRegister(None, 4096, ctypes.byref(h)) == 4
+    assert L.nexrHostRegister(ctypes.c_void_p(0x10000), 0, ctypes.byref(h)) == 4
+    assert L.nexrHostRegister(ctypes.c_void_p(0x10000), 4096, None) == 4
+    assert L.nexrHostDeregister(None) == 0
+    assert L.nexrHostDeregister(ctypes.c_void_p(0x1234)) == 5  # not a handle of this library
+    p = ctypes.c_void_p()
+    assert L.nexrHostMemAlloc(None, 4096) == 4
+    assert L.nexrHostMemAlloc(ctypes.byref(p), 0) == 4
+    assert L.nexrHostMemFree(None) == 0
+    assert L.nexrHostMemFree(ctypes.c_void_p(0x1234)) == 4   # not from nexrHostMemAlloc
+    assert L.nexrGetHostPathStats(None, 0) == 4
+    st = nexr.HostPathStats()
+    assert L.nexrGetHostPathStats(ctypes.byref(st), 1) == 0
+    assert nexr.host_path_stats()["calls"] == 0
+
+
 # Restatement of the reference struct (src/include/device.h:682-693, src/nccl.h.in:259-270), compiled
 # beside include/nexr.h as C11 and as C++17 (the reference's host code is C++): the two layouts must be
 # identical, field by field.

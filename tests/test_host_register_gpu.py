@@ -76,7 +76,13 @@ def test_registered_interior_pointers_zero_copy(hip, n):
         out[:] = np.nan
         guard_before = reg.buf[offs[2] - 64:offs[2]].copy()
         guard_after = reg.buf[offs[2] + 4 * n:offs[2] + 4 * n + 64].copy()
+        nexr.host_path_stats(reset=True)
         nexr.reduce_copy_ptrs([reg.base + offs[0], reg.base + offs[1]], [reg.base + offs[2]], n, 7, 0, host=True)
+        st = nexr.host_path_stats()
+        # which path ran: one zero-copy call, every buffer classified by the runtime's pointer query
+        # (the caller registered it, not the library), no staging copies
+        assert (st["calls"], st["zeroCopyCalls"], st["pointerQueries"], st["registeredHits"]) == (1, 1, 3, 0), st
+        assert st["copyNs"] == 0, st
         assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
         assert np.array_equal(reg.buf[offs[2] - 64:offs[2]], guard_before)
         assert np.array_equal(reg.buf[offs[2] + 4 * n:offs[2] + 4 * n + 64], guard_after)
@@ -130,3 +136,88 @@ def test_registered_rate_beside_pageable(hip):
     gbs = {k: 12 * n / v / 1e9 for k, v in secs.items()}
     print(f"registered {gbs[True]:.1f} GB/s, pageable {gbs[False]:.1f} GB/s")
     assert secs[True] <= secs[False] * 1.10, gbs
+
+
+HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, HIP_POINTER_ATTRIBUTE_RANGE_SIZE = 11, 12
+
+
+def test_runtime_reports_the_registered_range(hip):
+    """nexrReduceCopyHost reads a caller-registered buffer in place only when the range the runtime
+    reports for it (hipPointerGetAttribute RANGE_START_ADDR / RANGE_SIZE) covers the whole buffer.
+    This pins that the runtime answers those queries for an interior pointer of a hipHostRegister-ed
+    mapping, so the check is live (profiles/r05*_host_register_gpu_tests.txt records the values)."""
+    hip.hipPointerGetAttribute.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    hip.hipPointerGetAttribute.restype = ctypes.c_int
+    reg = Region(hip, 1 << 20)
+    try:
+        beg, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        p = reg.base + 12345
+        rc1 = hip.hipPointerGetAttribute(ctypes.byref(beg), HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, p)
+        rc2 = hip.hipPointerGetAttribute(ctypes.byref(size), HIP_POINTER_ATTRIBUTE_RANGE_SIZE, p)
+        print(f"rc {rc1} {rc2}: start {beg.value:#x} (mapping {reg.base:#x}), size {size.value} (mapping {1 << 20})")
+        assert rc1 == 0 and rc2 == 0
+        assert beg.value <= p and beg.value + size.value >= reg.base + (1 << 20)
+    finally:
+        reg.close()
+
+
+def test_library_registration_is_read_in_place_without_queries(hip):
+    """nexrHostRegister (ncclCommRegister's counterpart): the library records the range, so a call on
+    buffers inside it is classified from the cache with no runtime query and runs zero-copy; a range
+    inside it shares the entry; a partly overlapping one is refused; after the last deregistration
+    the same call stages the (now pageable) bytes and is still exact."""
+    nexr = importlib.import_module("nex-nccl_amd")
+    n = 1_000_003
+    gap = 4096 + 48
+    offs = [gap, 2 * gap + 4 * n, 3 * gap + 8 * n]
+    reg = Region(hip, offs[-1] + 4 * n + gap, register=False)
+    rng = np.random.default_rng(5)
+    a, b, out = (reg.f32(o, n) for o in offs)
+    _fill(rng, a)
+    _fill(rng, b)
+    ptrs = ([reg.base + offs[0], reg.base + offs[1]], [reg.base + offs[2]])
+    h = nexr.host_register(reg.base, reg.buf.size)
+    try:
+        inner = nexr.host_register(reg.base + 8192, 4096)  # inside: the same entry, one more reference
+        assert inner == h
+        nexr.host_deregister(inner)
+        with pytest.raises(nexr.NexrError) as e:  # straddles the entry's end
+            nexr.host_register(reg.base + reg.buf.size - 4096, 8192)
+        assert e.value.code == 5
+        out[:] = np.nan
+        nexr.host_path_stats(reset=True)
+        nexr.reduce_copy_ptrs(*ptrs, n, 7, 0, host=True)
+        st = nexr.host_path_stats()
+        assert (st["calls"], st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (1, 1, 3, 0), st
+        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+    finally:
+        nexr.host_deregister(h)
+    out[:] = np.nan
+    nexr.host_path_stats(reset=True)
+    nexr.reduce_copy_ptrs(*ptrs, n, 7, 0, host=True)
+    st = nexr.host_path_stats()
+    assert (st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (0, 0, 3), st
+    assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+
+
+def test_buffer_past_a_registered_range_is_staged(hip):
+    """A buffer that starts inside a registered range but runs past its end must not be read in place
+    (the device mapping covers only the range): the cache lookup misses, the runtime reports the
+    range, and the call stages the buffer instead (exact, zero-copy count 0)."""
+    nexr = importlib.import_module("nex-nccl_amd")
+    n = 1 << 20
+    reg = Region(hip, 4 * n * 4, register=False)
+    rng = np.random.default_rng(9)
+    a, b, out = reg.f32(0, n), reg.f32(4 * n, n), reg.f32(8 * n, n)
+    _fill(rng, a)
+    _fill(rng, b)
+    h = nexr.host_register(reg.base, 8 * n + 4 * n // 2)  # covers a, b and half of out
+    try:
+        out[:] = np.nan
+        nexr.host_path_stats(reset=True)
+        nexr.reduce_copy_ptrs([reg.base, reg.base + 4 * n], [reg.base + 8 * n], n, 7, 0, host=True)
+        st = nexr.host_path_stats()
+        assert (st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (0, 2, 1), st
+        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+    finally:
+        nexr.host_deregister(h)

@@ -1,0 +1,209 @@
+// Workgroups per CU, swept with an LDS reservation (tuning harness, not product code).
+//
+// tools/body_ab.hip (profiles/r05a_body_ab.txt) found the 16-bit K = 8 kernels 2-2.5 % faster held
+// to one 1024-lane workgroup per CU than at the two that their round-5 register count allows, with
+// the same code. Every trip of every configuration keeps K x U 16-B loads per lane in flight, so a
+// CU's bytes in flight are (workgroups per CU) x (lanes per workgroup) x K x U x 16: this sweeps that
+// count for each bench configuration and workgroup shape by launching the production kernel with a
+// dynamic LDS reservation of 160 KiB / n (rounded), which admits n workgroups per CU and changes
+// nothing in the code. Every variant is byte-checked against the configuration's production launch.
+// Blocks of launches over three rotating buffer sets, interleaved, order alternated.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNEXR_DT=6 tools/occupancy_ab.hip -o tools/occupancy_ab
+//   ./tools/occupancy_ab <blocks>
+#include "../nex-nccl_amd/csrc/nexr_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                     \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                    \
+    }                                                                             \
+  } while (0)
+
+using namespace nexr;
+
+__global__ void fill_bits(uint32_t* p, size_t n, uint64_t seed, uint32_t mask) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = (uint32_t)(z ^ (z >> 31)) & mask;
+  }
+}
+
+constexpr int kLdsPerCu = 160 * 1024;
+// Dynamic LDS that admits exactly n workgroups per CU (0: no reservation).
+int lds_for(int n) {
+  if (n <= 0) return 0;
+  const int hi = kLdsPerCu / n, lo = kLdsPerCu / (n + 1);
+  return ((lo + hi) / 2) & ~1023;
+}
+
+struct Var {
+  std::string name;
+  const void* fn;
+  int block;
+  int wgs;  // target workgroups per CU (0 = as the registers allow)
+  int esz;
+  uint64_t redArg;
+};
+struct Cfg {
+  const char* name;
+  int k;
+  size_t bytes;
+  uint32_t mask;
+  std::vector<Var> vars;
+};
+
+template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
+Var var(const char* geom, int wgs, uint64_t redArg = 0) {
+  char buf[128];
+  snprintf(buf, sizeof buf, "%s, %d WG/CU%s", geom, wgs > 0 ? wgs : 0, wgs > 0 ? "" : " (registers)");
+  return Var{buf, (const void*)&reduce_copy_kernel<D, OP, K, POL, IsMin, U, B>, B, wgs, 16 / Ty<D>::EPP, redArg};
+}
+
+int main(int argc, char** argv) {
+  const int blocks = argc > 1 ? atoi(argv[1]) : 10;
+  const uint32_t all = 0xffffffffu, fin = 0x3bff3bffu;
+  std::vector<Cfg> cfgs;
+  {
+    constexpr int D = nexrFloat32, OP = nexrDevSum, K = 2, P = kPolNt;
+    cfgs.push_back({"C2 fp32 sum K=2 256 MiB (nt/nt)", K, 256u << 20, fin,
+                    {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 4, 256>("U4 B256", 6),
+                     var<D, OP, K, P, false, 4, 256>("U4 B256", 5), var<D, OP, K, P, false, 4, 256>("U4 B256", 4),
+                     var<D, OP, K, P, false, 4, 256>("U4 B256", 3), var<D, OP, K, P, false, 4, 256>("U4 B256", 2),
+                     var<D, OP, K, P, false, 2, 512>("U2 B512", 0), var<D, OP, K, P, false, 2, 512>("U2 B512", 2)}});
+  }
+  {
+    constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8, P = kPolNt;
+    cfgs.push_back({"C3 fp16 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                    {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1),
+                     var<D, OP, K, P, false, 2, 512>("U2 B512", 0), var<D, OP, K, P, false, 2, 512>("U2 B512", 3),
+                     var<D, OP, K, P, false, 2, 512>("U2 B512", 2), var<D, OP, K, P, false, 4, 256>("U4 B256", 0),
+                     var<D, OP, K, P, false, 4, 256>("U4 B256", 6), var<D, OP, K, P, false, 4, 256>("U4 B256", 4)}});
+  }
+  {
+    constexpr int D = nexrBfloat16, OP = nexrDevSum, K = 8, P = kPolNt;
+    cfgs.push_back({"C3 bf16 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                    {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1),
+                     var<D, OP, K, P, false, 2, 512>("U2 B512", 2), var<D, OP, K, P, false, 4, 256>("U4 B256", 4)}});
+  }
+  {
+    constexpr int D = nexrInt8, OP = nexrDevMinMax, K = 4, P = kPolNtLoad;
+    cfgs.push_back({"C4 int8 max K=4 64 MiB (nt loads)", K, 64u << 20, all,
+                    {var<D, OP, K, P, false, 2, 512>("U2 B512", 0, 0x7f), var<D, OP, K, P, false, 2, 512>("U2 B512", 3, 0x7f),
+                     var<D, OP, K, P, false, 2, 512>("U2 B512", 2, 0x7f), var<D, OP, K, P, false, 2, 512>("U2 B512", 1, 0x7f),
+                     var<D, OP, K, P, false, 4, 256>("U4 B256", 0, 0x7f), var<D, OP, K, P, false, 4, 256>("U4 B256", 4, 0x7f)}});
+  }
+  {
+    constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4, P = kPolNtLoad;
+    cfgs.push_back({"C4 int32 min K=4 64 MiB (nt loads)", K, 64u << 20, all,
+                    {var<D, OP, K, P, true, 2, 512>("U2 B512", 0, 0x80000000ull),
+                     var<D, OP, K, P, true, 2, 512>("U2 B512", 3, 0x80000000ull),
+                     var<D, OP, K, P, true, 2, 512>("U2 B512", 2, 0x80000000ull),
+                     var<D, OP, K, P, true, 2, 512>("U2 B512", 1, 0x80000000ull)}});
+  }
+  const int R = 3, BLK = 6;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  printf("median (mean) us of %d blocks of %d launches over %d rotating sets, interleaved; fraction of 8 TB/s\n"
+         "from the median; 'vs first' = median over the first variant's (production) median; in flight = bytes of\n"
+         "loads outstanding per CU when every admitted lane has issued its trip\n\n", blocks, BLK, R);
+  for (size_t c = 0; c < cfgs.size(); c++) {
+    Cfg& cf = cfgs[c];
+    std::vector<RCParams> base(R);
+    std::vector<char*> owned;
+    for (int r = 0; r < R; r++) {
+      RCParams& p = base[r];
+      std::memset((void*)&p, 0, sizeof(p));
+      for (int s = 0; s < cf.k; s++) {
+        char* q;
+        CK(hipMalloc((void**)&q, cf.bytes));
+        fill_bits<<<2048, 256>>>((uint32_t*)q, cf.bytes / 4, 2000 + c * 64 + r * 16 + s, cf.mask);
+        p.src[s] = q;
+        owned.push_back(q);
+      }
+      CK(hipMalloc((void**)&p.dst[0], cf.bytes));
+      owned.push_back(p.dst[0]);
+      p.nDsts = 1;
+      p.nPacks = cf.bytes / 16;
+      p.head = 0;
+    }
+    for (Var& v : cf.vars) {
+      const int lds = lds_for(v.wgs);
+      if (lds > 64 * 1024) CK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    }
+    auto params = [&](const Var& v, int r) {
+      RCParams p = base[r];
+      p.nElts = cf.bytes / v.esz;
+      p.redArg = v.redArg;
+      return p;
+    };
+    for (const Var& v : cf.vars) {
+      const RCParams p = params(v, 0);
+      if (p.nElts * (uint64_t)v.esz != p.nPacks * 16 || p.nPacks % kTripPacks != 0 || cf.k > NEXR_MAX_SRCS) {
+        fprintf(stderr, "bad parameters for %s / %s\n", cf.name, v.name.c_str());
+        return 2;
+      }
+    }
+    CK(hipDeviceSynchronize());
+    const unsigned grid = (unsigned)(cf.bytes / 16 / kTripPacks);
+    auto launch = [&](size_t vi, int r) {
+      const Var& v = cf.vars[vi];
+      RCParams p = params(v, r);
+      void* args[] = {&p};
+      CK(hipLaunchKernel(v.fn, dim3(grid), dim3(v.block), args, lds_for(v.wgs), nullptr));
+    };
+    printf("%s\n", cf.name);
+    {  // bytes of every variant against the first (production) launch, set 0
+      std::vector<char> ref(cf.bytes), got(cf.bytes);
+      for (size_t vi = 0; vi < cf.vars.size(); vi++) {
+        CK(hipMemset(base[0].dst[0], 0x5a, cf.bytes));
+        launch(vi, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(vi ? got.data() : ref.data(), base[0].dst[0], cf.bytes, hipMemcpyDeviceToHost));
+        if (vi && memcmp(ref.data(), got.data(), cf.bytes) != 0) printf("  MISMATCH: %s\n", cf.vars[vi].name.c_str());
+      }
+    }
+    std::vector<std::vector<float>> us(cf.vars.size());
+    for (size_t vi = 0; vi < cf.vars.size(); vi++)
+      for (int w = 0; w < 2; w++) launch(vi, w % R);
+    for (int it = 0; it < blocks; it++)
+      for (size_t k = 0; k < cf.vars.size(); k++) {
+        const size_t vi = (it % 2) ? cf.vars.size() - 1 - k : k;
+        launch(vi, (it + BLK - 1) % R);
+        CK(hipEventRecord(e0));
+        for (int bb = 0; bb < BLK; bb++) launch(vi, (it + bb) % R);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        us[vi].push_back(ms * 1e3f / BLK);
+      }
+    const double alg = (double)(cf.k + 1) * cf.bytes;
+    double med0 = 0;
+    for (size_t vi = 0; vi < cf.vars.size(); vi++) {
+      std::vector<float> s = us[vi];
+      std::sort(s.begin(), s.end());
+      const double med = s[s.size() / 2];
+      double mean = 0;
+      for (float x : us[vi]) mean += x;
+      mean /= us[vi].size();
+      if (vi == 0) med0 = med;
+      printf("  %-30s lds %6d  %8.2f (%8.2f) us  %6.0f GB/s  %.4f  vs first %.4f\n", cf.vars[vi].name.c_str(),
+             lds_for(cf.vars[vi].wgs), med, mean, alg / med / 1e3, alg / med / 1e3 / 8000.0, med / med0);
+    }
+    for (char* q : owned) CK(hipFree(q));
+  }
+  return 0;
+}
