@@ -344,9 +344,21 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
   return nexrSuccess;
 }
 
+// maxGrid > 0 caps the grid (the kernel grid-strides): launches that read or write host memory over
+// PCIe use hostGrid() workgroups. With a one-shot grid every workgroup's loads are interleaved over the
+// whole transfer, so every workgroup's last load lands near its end and the writes start only then;
+// 32 workgroups keep ~1 MiB of reads in flight (more than the link's bandwidth x latency) and let the
+// early workgroups write while the others still read: +4-9 % at 1 MiB, +10-20 % at 4 MiB and +6-12 % at
+// 64 MiB per buffer over the one-shot grid (tools/zero_copy_sizes.py, profiles/r05f_zero_copy_grid.txt).
+uint64_t hostGrid() {
+  static const long g = envLong("NEXR_HOST_GRID", 32);
+  return g > 0 ? (uint64_t)g : 0;
+}
+
 nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, void* const* dsts,
                               size_t nElts, int datatype, int op, uint64_t redOpArg, int nPreOpSrcs,
-                              const uint64_t* preOpArgs, const void* prePtr, int postOp, hipStream_t stream) {
+                              const uint64_t* preOpArgs, const void* prePtr, int postOp, hipStream_t stream,
+                              uint64_t maxGrid = 0) {
   nexrResult_t r = validate(nSrcs, srcs, nDsts, dsts, nElts, datatype, op, redOpArg, nPreOpSrcs, preOpArgs);
   if (r != nexrSuccess) return r;
   if (nElts == 0 || nDsts == 0) return nexrSuccess;  // common_kernel.h:288-289: nothing to store
@@ -357,7 +369,9 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   fillParams(p, c.nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, c.nPreOp, preOpArgs, c.prePtr, c.postOp);
   Geometry g;
   const int pol = pickPolicy((uint64_t)(c.nSrcs + nDsts) * nElts * esz);
-  r = pickGeometry(workgroupsFor(p, c.nSrcs, c.dt, pol), pol, block_for(c.dt, c.nSrcs, pol), &g);
+  uint64_t wgs = workgroupsFor(p, c.nSrcs, c.dt, pol);
+  if (maxGrid > 0 && wgs > maxGrid) wgs = maxGrid;
+  r = pickGeometry(wgs, pol, block_for(c.dt, c.nSrcs, pol), &g);
   if (r != nexrSuccess) return r;
   NEXR_HIP(launchDt(c.dt, p, c.op, c.nSrcs, g, stream));
   return nexrSuccess;
@@ -802,7 +816,7 @@ nexrResult_t reduceCopyHostTeam(int nSrcs, const void* const* srcs, const bool* 
       if (pdst[d]) ddst[m++] = (char*)zdst[d] + e0 * esz;
     if (outStaged) ddst[m++] = st->dev + slot + outOffset();
     nexrResult_t rr = reduceCopyDevice(nSrcs, dsrc, m, ddst, n, datatype, op, redOpArg, nPreOpSrcs, preOpArgs,
-                                       nullptr, postOp, s);
+                                       nullptr, postOp, s, hostGrid());
     if (rr != nexrSuccess) return rr;
     NEXR_HIP(hipEventRecord(st->done[c % kPinnedSlots], s));
     return nexrSuccess;
@@ -1044,7 +1058,7 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
   if (nPinned == nSrcs + nDsts) {
     gHpZeroCopy.fetch_add(1, std::memory_order_relaxed);
     r = reduceCopyDevice(nSrcs, zsrc, nDsts, zdst, nElts, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs,
-                         nullptr, postOp, s);
+                         nullptr, postOp, s, hostGrid());
     const uint64_t tc2 = nowNs();
     gHpLaunchNs.fetch_add(tc2 - tc1, std::memory_order_relaxed);
     if (r != nexrSuccess) return r;
@@ -1103,7 +1117,7 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
     char* staged = base + chunkBytes * nSrcs;
     if (anyPageableDst) ddst[m++] = staged;
     r = reduceCopyDevice(nSrcs, dsrc, m, ddst, n, datatype, devRedOp, redOpArg, nPreOpSrcs, preOpArgs, nullptr,
-                         postOp, s);
+                         postOp, s, nPinned > 0 ? hostGrid() : 0);
     if (r != nexrSuccess) return r;
     NEXR_HIP(hipEventRecord(st->kernelDone[slot], s));
     NEXR_HIP(hipStreamWaitEvent(st->out, st->kernelDone[slot], 0));

@@ -23,6 +23,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="", help="comma-separated subset of the shape names")
+    ap.add_argument("--mib", default="", help="comma-separated buffer sizes in KiB")
+    args = ap.parse_args()
     import torch
     torch.cuda.init()
     nexr = importlib.import_module("nex-nccl_amd")
@@ -35,9 +40,13 @@ def main():
         h = nexr.host_register(a.ctypes.data, a.nbytes)
         regions.append((m, a, h))
     shapes = {"copy K1 M1": (1, 1), "reduce K2 M1": (2, 1), "recvReduceCopySend K2 M2": (2, 2)}
+    if args.shapes:
+        shapes = {k: v for k, v in shapes.items() if k.split()[0] in args.shapes.split(",")}
+    sizes = [int(x) << 10 for x in args.mib.split(",")] if args.mib else [256 << 10, 1 << 20, 2 << 20, 4 << 20,
+                                                                         16 << 20, 64 << 20]
     out = []
     for name, (k, m_) in shapes.items():
-        for b in [256 << 10, 1 << 20, 2 << 20, 4 << 20, 16 << 20, 64 << 20]:
+        for b in sizes:
             n = b // 4
 
             def call(i):
@@ -62,7 +71,7 @@ def main():
                 dt = (time.perf_counter() - t0) / reps
                 st = nexr.host_path_stats(reset=True)
                 calls = max(1, st["calls"])
-                row = {"shape": name, "bytes_per_buffer": b, "threads": threads, "us_per_call": round(dt * 1e6, 1),
+                row = {"shape": name, "grid": os.environ.get("NEXR_GRID", "one-shot"), "bytes_per_buffer": b, "threads": threads, "us_per_call": round(dt * 1e6, 1),
                        "GBps": round(threads * (k + m_) * b / dt / 1e9, 1),
                        "zero_copy": st["zeroCopyCalls"] == st["calls"],
                        **{f"{x}_us": round(st[x + "Ns"] / calls / 1e3, 2) for x in ("classify", "launch", "wait")}}
