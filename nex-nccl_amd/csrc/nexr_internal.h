@@ -128,27 +128,32 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 //     B = 512 — +0.9 % on average over 9 datatypes x {sum, min} on four boxes, never below -0.7 %
 //     (tools/geom_sweep.hip, profiles/r02_geom_sweep_*.log; int8 min/max/prod +1-2 %);
 //   - K = 4 with non-temporal loads and stores (>= 512 MiB streamed), every type but fp16: U = 1,
-//     B = 1024 — +0.5-4 % (+2 % on average) on the same boxes; fp16 alone is mixed there.
+//     B = 1024 — +0.5-4 % (+2 % on average) on the same boxes; fp16 alone is mixed there;
+//   - K >= 6 with non-temporal loads and stores, every type (round 5): U = 1, B = 1024 at one
+//     workgroup per CU (lds_for) — 1.3-2.8 % faster than U = 4, B = 256 for fp32 / uint32 / fp64 /
+//     int8 at K = 8 and fp32 / fp16 at K = 6, byte-identical; at 32 MiB per buffer (nt loads only)
+//     3.8 % slower, so only under the nt-store policy (tools/occupancy_ab.hip wide,
+//     profiles/r05i_occupancy_wide.txt).
 // K = 2 keeps the default everywhere (U = 1 loses 10-13 %, U = 2 loses 1-5 %).
 constexpr int kTripPacks = 1024;
 __host__ __device__ constexpr int unroll_for(int dt, int k, int pol) {
   return ((dt == nexrFloat16 || dt == nexrBfloat16) && k >= 8) ? 1
+         : (k >= 6 && pol == 3)                                 ? 1
          : (k == 4 && pol == 1)                                 ? 2
          : (k == 4 && pol == 3 && dt != nexrFloat16)            ? 1
                                                                 : 4;
 }
 __host__ __device__ constexpr int block_for(int dt, int k, int pol) { return kTripPacks / unroll_for(dt, k, pol); }
-// Workgroups per CU: the registers of the round-5 kernels admit two 1024-lane workgroups of the 16-bit
-// K = 8 geometry per CU (256 KiB of loads in flight per CU); one is 1.4-3.0 % faster on four boxes,
-// for fp16 and bf16 alike (tools/body_ab.hip, tools/occupancy_ab.hip, tools/data_ab.hip;
-// profiles/r05a_body_ab.txt, r05b_occupancy_ab.txt, r05c_data_ab.txt). The launch reserves this many
-// bytes of dynamic LDS (the kernel never touches it) so that only one fits in a CU's 160 KiB. Every
-// other geometry runs as its registers allow: C2 is flat from 2 to 8 workgroups per CU, C4 from 2 to 4.
+// Workgroups per CU: the registers of the round-5 kernels admit two 1024-lane workgroups of the K >= 6
+// geometry per CU (2 x K x 16 KiB of loads in flight per CU); one is 1.4-3.0 % faster on four boxes, for
+// fp16 and bf16 alike at K = 8 (tools/body_ab.hip, tools/occupancy_ab.hip, tools/data_ab.hip;
+// profiles/r05a_body_ab.txt, r05b_occupancy_ab.txt, r05c_data_ab.txt), and the K >= 6 geometry above
+// was measured at one. The launch reserves this many bytes of dynamic LDS (the kernel never touches
+// it) so that only one fits in a CU's 160 KiB. Every other geometry runs as its registers allow: C2
+// is flat from 2 to 8 workgroups per CU, C4 from 2 to 4.
 constexpr int kLdsOneWorkgroupPerCu = 120 * 1024;
 __host__ __device__ constexpr int lds_for(int dt, int k, int pol) {
-  return unroll_for(dt, k, pol) == 1 && block_for(dt, k, pol) == 1024 && (dt == nexrFloat16 || dt == nexrBfloat16)
-             ? kLdsOneWorkgroupPerCu
-             : 0;
+  return unroll_for(dt, k, pol) == 1 && block_for(dt, k, pol) == 1024 && k >= 6 ? kLdsOneWorkgroupPerCu : 0;
 }
 
 }  // namespace nexr

@@ -214,6 +214,14 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     for k in (3, 5):
         info = nexr.query_launch(k4[:3] + [0x50000000] * (k - 3), [0x60000000], 64 << 20, 7)
         assert (info.block, info.packsPerLane) == (256, 4)
+    # K >= 6 under the nt-store policy (>= 512 MiB streamed): 1 x 1024 for every type (round 5); below
+    # it the default, except 16-bit K = 8, which is 1 x 1024 at every size
+    k8 = [0x10000000 * (i + 1) for i in range(8)]
+    for k, dt, n, want in ((6, 7, 64 << 20, (16384, 1024, 1, 3)), (8, 2, 64 << 20, (16384, 1024, 1, 3)),
+                           (7, 8, 32 << 20, (16384, 1024, 1, 3)), (8, 7, 4 << 20, (1024, 256, 4, 1)),
+                           (6, 0, 1 << 20, (64, 256, 4, 0)), (8, 9, 1 << 20, (128, 1024, 1, 0))):
+        info = nexr.query_launch(k8[:k], [0x90000000], n, dt)
+        assert (info.grid, info.block, info.packsPerLane, info.policy) == want, (k, dt, n)
     # head/body/tail split for a shared 4-B phase: the head brings dst0 to its next 128-B boundary
     # (31 fp32 elements), then 17 packs, then 1 tail element
     info = nexr.query_launch([0x1004, 0x2004], [0x3004], 100, 7)

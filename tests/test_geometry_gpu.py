@@ -146,3 +146,22 @@ def test_k4_geometry_random_large_calls(nexr, oracle, dev):
         assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (case, mg.DT_NAMES[dt], name, n, offs)
         del srcs, exp, got
         torch.cuda.empty_cache()
+
+
+# ---- K >= 6 under the nt-store policy: one pack x 1024 lanes, one workgroup per CU (round 5) ----------
+@pytest.mark.parametrize("dt,k,op,name,buf_mib", [(mg.F32, 6, mg.SUM, "sum", 88), (mg.I32, 8, mg.MINMAX, "max", 60),
+                                                  (mg.F64, 7, mg.SUM, "sum", 68)])
+def test_wide_fan_in_nt_store_geometry_edges(nexr, oracle, dev, dt, k, op, name, buf_mib):
+    esz = np.dtype(mg.STORE[dt]).itemsize
+    base = buf_mib * MIB // esz
+    arg = mg.minmax_arg(dt, name == "max") if op == mg.MINMAX else 0
+    for n, offs in ((base + 16 // esz * 1024 * 2 + 3, None), (base - 5, [esz] * (k + 1))):
+        srcs = mg.gen_inputs(dt, k, n, 5100 + n % 1013, special=True)
+        info = nexr.query_launch([0x1000000 * (i + 1) + (offs[i] if offs else 0) for i in range(k)],
+                                 [0x9000000 + (offs[k] if offs else 0)], n, dt)
+        assert (info.policy, info.block, info.packsPerLane) == (3, 1024, 1), (n, offs)
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
+        got = _run(nexr, srcs, dt, op, arg, offs)
+        assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)
+        del srcs, exp, got
+        torch.cuda.empty_cache()

@@ -73,8 +73,52 @@ Var var(const char* geom, int wgs, uint64_t redArg = 0) {
 
 int main(int argc, char** argv) {
   const int blocks = argc > 1 ? atoi(argv[1]) : 10;
+  // group "bench" (default): the bench configurations; "wide": fan-in 6 and 8 of every element size,
+  // production geometry against one 1024-lane workgroup per CU
+  const std::string group = argc > 2 ? argv[2] : "bench";
   const uint32_t all = 0xffffffffu, fin = 0x3bff3bffu;
   std::vector<Cfg> cfgs;
+  if (group == "wide") {
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 8, P = kPolNt;
+      cfgs.push_back({"fp32 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1),
+                       var<D, OP, K, P, false, 1, 1024>("U1 B1024", 0), var<D, OP, K, P, false, 2, 512>("U2 B512", 2)}});
+    }
+    {
+      constexpr int D = nexrUint32, OP = nexrDevSum, K = 8, P = kPolNt;
+      cfgs.push_back({"uint32 sum K=8 256 MiB (nt/nt)", K, 256u << 20, all,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1)}});
+    }
+    {
+      constexpr int D = nexrFloat64, OP = nexrDevSum, K = 8, P = kPolNt;
+      cfgs.push_back({"fp64 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1)}});
+    }
+    {
+      constexpr int D = nexrInt8, OP = nexrDevMinMax, K = 8, P = kPolNt;
+      cfgs.push_back({"int8 max K=8 256 MiB (nt/nt)", K, 256u << 20, all,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0, 0x7f),
+                       var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1, 0x7f)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 6, P = kPolNt;
+      cfgs.push_back({"fp32 sum K=6 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1),
+                       var<D, OP, K, P, false, 2, 512>("U2 B512", 2)}});
+    }
+    {
+      constexpr int D = nexrFloat16, OP = nexrDevSum, K = 6, P = kPolNt;
+      cfgs.push_back({"fp16 sum K=6 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 8, P = kPolNtLoad;
+      cfgs.push_back({"fp32 sum K=8 32 MiB (nt loads)", K, 32u << 20, fin,
+                      {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1)}});
+    }
+  }
+  if (group == "bench") {
   {
     constexpr int D = nexrFloat32, OP = nexrDevSum, K = 2, P = kPolNt;
     cfgs.push_back({"C2 fp32 sum K=2 256 MiB (nt/nt)", K, 256u << 20, fin,
@@ -111,6 +155,7 @@ int main(int argc, char** argv) {
                      var<D, OP, K, P, true, 2, 512>("U2 B512", 3, 0x80000000ull),
                      var<D, OP, K, P, true, 2, 512>("U2 B512", 2, 0x80000000ull),
                      var<D, OP, K, P, true, 2, 512>("U2 B512", 1, 0x80000000ull)}});
+  }
   }
   const int R = 3, BLK = 6;
   hipEvent_t e0, e1;
