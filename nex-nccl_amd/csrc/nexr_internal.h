@@ -117,43 +117,50 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 #undef NEXR_DECLARE_BATCH
 
 // Workgroup geometry per (datatype, fan-in, cache policy): U packs per lane x B lanes per workgroup,
-// always one trip of kTripPacks 16-B packs (16 KiB) per buffer, so the grid is nPacks / kTripPacks
-// whatever the geometry. U = 4, B = 256 is the default (round-1 steady-state sweeps over U in
-// {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8: profiles/r01_tune_*.log,
-// r01_skew.log, r01s2_geom_*.log). Three exceptions, each measured in one process against the default
-// on several boxes with byte-identical outputs:
-//   - 16-bit floats, K >= 8 (any size): U = 1, B = 1024 — fp16 399.9 vs 407.9 us, bf16 394.9 vs
-//     402.0 us at C3 in same-box A/Bs alternated six times (profiles/r01s3_*_geometry_ab.txt);
+// and whether the launch holds the kernel to one workgroup per CU (lds_for). A workgroup owns one trip
+// of U x B packs of every buffer, so the one-shot grid is nPacks / (U x B). U = 4, B = 256 is the default
+// (round-1 steady-state sweeps over U in {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8:
+// profiles/r01_tune_*.log, r01_skew.log, r01s2_geom_*.log). The exceptions, each measured in one process
+// against the alternatives on several boxes with byte-identical outputs:
 //   - K = 4 with non-temporal loads and cached stores (64-512 MiB streamed, C4's regime): U = 2,
 //     B = 512 — +0.9 % on average over 9 datatypes x {sum, min} on four boxes, never below -0.7 %
-//     (tools/geom_sweep.hip, profiles/r02_geom_sweep_*.log; int8 min/max/prod +1-2 %);
-//   - K = 4 with non-temporal loads and stores (>= 512 MiB streamed), every type but fp16: U = 1,
-//     B = 1024 — +0.5-4 % (+2 % on average) on the same boxes; fp16 alone is mixed there;
-//   - K >= 6 with non-temporal loads and stores, every type (round 5): U = 1, B = 1024 at one
-//     workgroup per CU (lds_for) — 1.3-2.8 % faster than U = 4, B = 256 for fp32 / uint32 / fp64 /
-//     int8 at K = 8 and fp32 / fp16 at K = 6, byte-identical; at 32 MiB per buffer (nt loads only)
-//     3.8 % slower, so only under the nt-store policy (tools/occupancy_ab.hip wide,
-//     profiles/r05i_occupancy_wide.txt).
-// K = 2 keeps the default everywhere (U = 1 loses 10-13 %, U = 2 loses 1-5 %).
-constexpr int kTripPacks = 1024;
-__host__ __device__ constexpr int unroll_for(int dt, int k, int pol) {
-  return ((dt == nexrFloat16 || dt == nexrBfloat16) && k >= 8) ? 1
-         : (k >= 6 && pol == 3)                                 ? 1
-         : (k == 4 && pol == 1)                                 ? 2
-         : (k == 4 && pol == 3 && dt != nexrFloat16)            ? 1
-                                                                : 4;
+//     (profiles/r02_geom_sweep_*.log); at one or two workgroups per CU 1-18 % slower
+//     (profiles/r05l_occupancy_k8lanes.txt);
+//   - the nt-store policy (>= 512 MiB streamed), where a CU's loads in flight are the lever (round 5,
+//     tools/occupancy_ab.hip, profiles/r05b_occupancy_ab.txt, r05i_occupancy_wide.txt,
+//     r05k_occupancy_k8shape.txt, r05l_occupancy_k8lanes.txt): the fastest point is about 64 KiB of
+//     loads in flight per CU, i.e. 4096 / K lanes with one pack each, at ONE workgroup per CU
+//       K = 4 (every type but fp16, mixed there): U = 1, B = 1024 — 4.2 % faster than the two
+//         workgroups per CU its registers allow, and +0.5-4 % over 4 x 256 (profiles/r02_geom_sweep_*);
+//       K >= 6: U = 1, B = 512 — fp16 K = 8 2.5-2.7 % and fp32 K = 8 3.6 % faster than 1 x 1024, fp32
+//         K = 6 1.3 %; 256 lanes are 10-20 % slower, 384 or 640 lanes 2 % slower;
+//       bf16, K >= 6: U = 1, B = 1024 — its fold is ~15x the VALU of fp16's, and 512 lanes per CU do not
+//         hide it (2.9 % slower than 1024);
+//   - 16-bit floats, K >= 8, below the nt-store policy: U = 1, B = 1024 at one workgroup per CU (rounds 1
+//     and 5: fp16 399.9 vs 407.9 us, bf16 394.9 vs 402.0 us at C3 against 4 x 256,
+//     profiles/r01s3_*_geometry_ab.txt).
+// K = 2 keeps the default everywhere (U = 1 loses 10-13 %, U = 2 loses 1-5 %; 2 to 8 workgroups per CU
+// are flat, profiles/r05b_occupancy_ab.txt).
+constexpr int kTripPacks = 1024;  // the default trip (4 x 256)
+struct Shape {
+  int u, b;
+  bool oneWgPerCu;
+};
+__host__ __device__ constexpr Shape shape_for(int dt, int k, int pol) {
+  const bool half = dt == nexrFloat16 || dt == nexrBfloat16;
+  return (pol == 3 && k >= 6)                       ? Shape{1, dt == nexrBfloat16 ? 1024 : 512, true}
+         : (half && k >= 8)                         ? Shape{1, 1024, true}
+         : (k == 4 && pol == 1)                     ? Shape{2, 512, false}
+         : (k == 4 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}
+                                                    : Shape{4, 256, false};
 }
-__host__ __device__ constexpr int block_for(int dt, int k, int pol) { return kTripPacks / unroll_for(dt, k, pol); }
-// Workgroups per CU: the registers of the round-5 kernels admit two 1024-lane workgroups of the K >= 6
-// geometry per CU (2 x K x 16 KiB of loads in flight per CU); one is 1.4-3.0 % faster on four boxes, for
-// fp16 and bf16 alike at K = 8 (tools/body_ab.hip, tools/occupancy_ab.hip, tools/data_ab.hip;
-// profiles/r05a_body_ab.txt, r05b_occupancy_ab.txt, r05c_data_ab.txt), and the K >= 6 geometry above
-// was measured at one. The launch reserves this many bytes of dynamic LDS (the kernel never touches
-// it) so that only one fits in a CU's 160 KiB. Every other geometry runs as its registers allow: C2
-// is flat from 2 to 8 workgroups per CU, C4 from 2 to 4.
+__host__ __device__ constexpr int unroll_for(int dt, int k, int pol) { return shape_for(dt, k, pol).u; }
+__host__ __device__ constexpr int block_for(int dt, int k, int pol) { return shape_for(dt, k, pol).b; }
+// One workgroup per CU: the launch reserves this many bytes of dynamic LDS (the kernel never touches
+// it), so that only one fits in a CU's 160 KiB whatever the kernel's registers would admit.
 constexpr int kLdsOneWorkgroupPerCu = 120 * 1024;
 __host__ __device__ constexpr int lds_for(int dt, int k, int pol) {
-  return unroll_for(dt, k, pol) == 1 && block_for(dt, k, pol) == 1024 && k >= 6 ? kLdsOneWorkgroupPerCu : 0;
+  return shape_for(dt, k, pol).oneWgPerCu ? kLdsOneWorkgroupPerCu : 0;
 }
 
 }  // namespace nexr

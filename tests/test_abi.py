@@ -190,14 +190,15 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     assert info.grid == 0xFFFFFFFF // 256
     info = nexr.query_launch([0x1000, 0x2001], [0x3000], 1 << 32, 0)
     assert info.unaligned == 1 and info.grid == (1 << 32) // 16 // 4 // 256
-    # fp16 K=8 (block 1024): a 16 GiB body would need 2^20 workgroups -> under the 2^22 cap
+    # fp16 K=8 under the nt-store policy (block 512): a 16 GiB body needs 2^21 workgroups -> under the
+    # 2^23 cap
     srcs = [0x10000 * (i + 1) for i in range(8)]
     info = nexr.query_launch(srcs, [0x100000], 8 << 30, 6)
-    assert info.generic == 0 and info.block == 1024 and info.packsPerLane == 1
-    assert info.grid == (8 << 30) * 2 // 16 // 1024 and info.grid * info.block <= 0xFFFFFFFF
+    assert info.generic == 0 and info.block == 512 and info.packsPerLane == 1
+    assert info.grid == (8 << 30) * 2 // 16 // 512 and info.grid * info.block <= 0xFFFFFFFF
     # fp16 K=8 with mixed phases at 2^33 elements: packed like the aligned call above
     info = nexr.query_launch([0x10000 * (i + 1) + (i & 1) * 2 for i in range(8)], [0x100000], 1 << 33, 6)
-    assert (info.generic, info.unaligned) == (0, 1) and info.grid == (1 << 34) // 16 // 1024
+    assert (info.generic, info.unaligned) == (0, 1) and info.grid == (1 << 34) // 16 // 512
     # C2 geometry: 256 MiB fp32 K=2, U=4 packs per lane, one 16 KiB trip per workgroup, nt loads
     info = nexr.query_launch([0x10000000, 0x20000000], [0x30000000], 64 << 20, 7)
     assert (info.grid, info.block, info.packsPerLane, info.policy) == (16384, 256, 4, 3)
@@ -214,12 +215,14 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     for k in (3, 5):
         info = nexr.query_launch(k4[:3] + [0x50000000] * (k - 3), [0x60000000], 64 << 20, 7)
         assert (info.block, info.packsPerLane) == (256, 4)
-    # K >= 6 under the nt-store policy (>= 512 MiB streamed): 1 x 1024 for every type (round 5); below
-    # it the default, except 16-bit K = 8, which is 1 x 1024 at every size
+    # K >= 6 under the nt-store policy (>= 512 MiB streamed): 1 x 512 for every type but bf16, 1 x 1024
+    # for bf16 (round 5); below it the default, except 16-bit K = 8, which is 1 x 1024 at every size
     k8 = [0x10000000 * (i + 1) for i in range(8)]
-    for k, dt, n, want in ((6, 7, 64 << 20, (16384, 1024, 1, 3)), (8, 2, 64 << 20, (16384, 1024, 1, 3)),
-                           (7, 8, 32 << 20, (16384, 1024, 1, 3)), (8, 7, 4 << 20, (1024, 256, 4, 1)),
-                           (6, 0, 1 << 20, (64, 256, 4, 0)), (8, 9, 1 << 20, (128, 1024, 1, 0))):
+    for k, dt, n, want in ((6, 7, 64 << 20, (32768, 512, 1, 3)), (8, 2, 64 << 20, (32768, 512, 1, 3)),
+                           (7, 8, 32 << 20, (32768, 512, 1, 3)), (8, 9, 128 << 20, (16384, 1024, 1, 3)),
+                           (6, 9, 128 << 20, (16384, 1024, 1, 3)), (8, 6, 128 << 20, (32768, 512, 1, 3)),
+                           (8, 7, 4 << 20, (1024, 256, 4, 1)), (6, 0, 1 << 20, (64, 256, 4, 0)),
+                           (8, 9, 1 << 20, (128, 1024, 1, 0)), (8, 6, 8 << 20, (1024, 1024, 1, 1))):
         info = nexr.query_launch(k8[:k], [0x90000000], n, dt)
         assert (info.grid, info.block, info.packsPerLane, info.policy) == want, (k, dt, n)
     # head/body/tail split for a shared 4-B phase: the head brings dst0 to its next 128-B boundary

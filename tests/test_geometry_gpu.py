@@ -148,7 +148,7 @@ def test_k4_geometry_random_large_calls(nexr, oracle, dev):
         torch.cuda.empty_cache()
 
 
-# ---- K >= 6 under the nt-store policy: one pack x 1024 lanes, one workgroup per CU (round 5) ----------
+# ---- K >= 6 under the nt-store policy: one pack x 512 lanes, one workgroup per CU (round 5) -----------
 @pytest.mark.parametrize("dt,k,op,name,buf_mib", [(mg.F32, 6, mg.SUM, "sum", 88), (mg.I32, 8, mg.MINMAX, "max", 60),
                                                   (mg.F64, 7, mg.SUM, "sum", 68)])
 def test_wide_fan_in_nt_store_geometry_edges(nexr, oracle, dev, dt, k, op, name, buf_mib):
@@ -159,9 +159,21 @@ def test_wide_fan_in_nt_store_geometry_edges(nexr, oracle, dev, dt, k, op, name,
         srcs = mg.gen_inputs(dt, k, n, 5100 + n % 1013, special=True)
         info = nexr.query_launch([0x1000000 * (i + 1) + (offs[i] if offs else 0) for i in range(k)],
                                  [0x9000000 + (offs[k] if offs else 0)], n, dt)
-        assert (info.policy, info.block, info.packsPerLane) == (3, 1024, 1), (n, offs)
+        assert (info.policy, info.block, info.packsPerLane) == (3, 512, 1), (n, offs)
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
         got = _run(nexr, srcs, dt, op, arg, offs)
         assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)
         del srcs, exp, got
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("dt,k", [(mg.F16, 8), (mg.BF16, 6)])
+def test_16bit_wide_fan_in_nt_store_geometry(nexr, oracle, dev, dt, k):
+    """fp16 K = 8 at >= 512 MiB streamed runs 512 lanes, bf16 K >= 6 1024 lanes (its fold's VALU), both one
+    pack per lane at one workgroup per CU; a size just past a trip boundary, against the oracle."""
+    n = 40 * MIB + 8 * 512 * 2 + 3  # 80 MiB per buffer: >= 512 MiB streamed for K >= 6
+    srcs = mg.gen_inputs(dt, k, n, 6100 + k, special=True)
+    info = nexr.query_launch([0x1000000 * (i + 1) for i in range(k)], [0x9000000], n, dt)
+    assert (info.policy, info.block, info.packsPerLane) == (3, 512 if dt == mg.F16 else 1024, 1)
+    exp = oracle.reduce_copy(srcs, 1, dt, mg.SUM, 0, threads=16)[0]
+    assert mg.canon_bytes(dt, _run(nexr, srcs, dt, mg.SUM, 0)) == mg.canon_bytes(dt, exp)

@@ -54,6 +54,7 @@ struct Var {
   int block;
   int wgs;  // target workgroups per CU (0 = as the registers allow)
   int esz;
+  int trip;  // packs per workgroup trip (U x B)
   uint64_t redArg;
 };
 struct Cfg {
@@ -68,7 +69,7 @@ template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
 Var var(const char* geom, int wgs, uint64_t redArg = 0) {
   char buf[128];
   snprintf(buf, sizeof buf, "%s, %d WG/CU%s", geom, wgs > 0 ? wgs : 0, wgs > 0 ? "" : " (registers)");
-  return Var{buf, (const void*)&reduce_copy_kernel<D, OP, K, POL, IsMin, U, B>, B, wgs, 16 / Ty<D>::EPP, redArg};
+  return Var{buf, (const void*)&reduce_copy_kernel<D, OP, K, POL, IsMin, U, B>, B, wgs, 16 / Ty<D>::EPP, U * B, redArg};
 }
 
 int main(int argc, char** argv) {
@@ -116,6 +117,60 @@ int main(int argc, char** argv) {
       constexpr int D = nexrFloat32, OP = nexrDevSum, K = 8, P = kPolNtLoad;
       cfgs.push_back({"fp32 sum K=8 32 MiB (nt loads)", K, 32u << 20, fin,
                       {var<D, OP, K, P, false, 4, 256>("U4 B256", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1)}});
+    }
+  }
+  if (group == "k8shape") {  // the 16-bit K = 8 workgroup shape at one and more workgroups per CU
+    constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8, P = kPolNt;
+    cfgs.push_back({"fp16 sum K=8 256 MiB (nt/nt): workgroup shape x workgroups per CU", K, 256u << 20, fin,
+                    {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1), var<D, OP, K, P, false, 1, 512>("U1 B512", 1),
+                     var<D, OP, K, P, false, 1, 512>("U1 B512", 2), var<D, OP, K, P, false, 1, 512>("U1 B512", 3),
+                     var<D, OP, K, P, false, 2, 512>("U2 B512", 1), var<D, OP, K, P, false, 1, 256>("U1 B256", 2),
+                     var<D, OP, K, P, false, 1, 256>("U1 B256", 4), var<D, OP, K, P, false, 1, 256>("U1 B256", 6),
+                     var<D, OP, K, P, false, 2, 256>("U2 B256", 2), var<D, OP, K, P, false, 1, 768>("U1 B768", 1)}});
+    constexpr int D2 = nexrFloat32, K2 = 2;
+    cfgs.push_back({"fp32 sum K=2 256 MiB (nt/nt): workgroup shape x workgroups per CU", K2, 256u << 20, fin,
+                    {var<D2, OP, K2, P, false, 4, 256>("U4 B256", 0), var<D2, OP, K2, P, false, 2, 1024>("U2 B1024", 2),
+                     var<D2, OP, K2, P, false, 4, 1024>("U4 B1024", 1), var<D2, OP, K2, P, false, 4, 512>("U4 B512", 2),
+                     var<D2, OP, K2, P, false, 8, 256>("U8 B256", 0), var<D2, OP, K2, P, false, 8, 256>("U8 B256", 4)}});
+  }
+  if (group == "k8lanes") {  // lanes per CU at K >= 6: one workgroup of B lanes (U = 1) per CU
+    {
+      constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8, P = kPolNt;
+      cfgs.push_back({"fp16 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1), var<D, OP, K, P, false, 1, 512>("U1 B512", 1),
+                       var<D, OP, K, P, false, 1, 256>("U1 B256", 1), var<D, OP, K, P, false, 1, 384>("U1 B384", 1),
+                       var<D, OP, K, P, false, 1, 640>("U1 B640", 1), var<D, OP, K, P, false, 2, 256>("U2 B256", 1),
+                       var<D, OP, K, P, false, 1, 128>("U1 B128", 2), var<D, OP, K, P, false, 1, 128>("U1 B128", 4)}});
+    }
+    {
+      constexpr int D = nexrBfloat16, OP = nexrDevSum, K = 8, P = kPolNt;
+      cfgs.push_back({"bf16 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1), var<D, OP, K, P, false, 1, 512>("U1 B512", 1),
+                       var<D, OP, K, P, false, 1, 256>("U1 B256", 1)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 8, P = kPolNt;
+      cfgs.push_back({"fp32 sum K=8 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1), var<D, OP, K, P, false, 1, 512>("U1 B512", 1),
+                       var<D, OP, K, P, false, 1, 256>("U1 B256", 1)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 6, P = kPolNt;
+      cfgs.push_back({"fp32 sum K=6 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1), var<D, OP, K, P, false, 1, 512>("U1 B512", 1),
+                       var<D, OP, K, P, false, 1, 256>("U1 B256", 1)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 4, P = kPolNt;
+      cfgs.push_back({"fp32 sum K=4 256 MiB (nt/nt)", K, 256u << 20, fin,
+                      {var<D, OP, K, P, false, 1, 1024>("U1 B1024", 0), var<D, OP, K, P, false, 1, 1024>("U1 B1024", 1),
+                       var<D, OP, K, P, false, 1, 512>("U1 B512", 1), var<D, OP, K, P, false, 1, 512>("U1 B512", 2)}});
+    }
+    {
+      constexpr int D = nexrInt8, OP = nexrDevMinMax, K = 4, P = kPolNtLoad;
+      cfgs.push_back({"C4 int8 max K=4 64 MiB (nt loads)", K, 64u << 20, all,
+                      {var<D, OP, K, P, false, 2, 512>("U2 B512", 0, 0x7f), var<D, OP, K, P, false, 1, 512>("U1 B512", 1, 0x7f),
+                       var<D, OP, K, P, false, 1, 512>("U1 B512", 2, 0x7f), var<D, OP, K, P, false, 2, 512>("U2 B512", 2, 0x7f)}});
     }
   }
   if (group == "bench") {
@@ -202,12 +257,12 @@ int main(int argc, char** argv) {
       }
     }
     CK(hipDeviceSynchronize());
-    const unsigned grid = (unsigned)(cf.bytes / 16 / kTripPacks);
+    // one-shot grid: one workgroup per trip of the variant's own size
     auto launch = [&](size_t vi, int r) {
       const Var& v = cf.vars[vi];
       RCParams p = params(v, r);
       void* args[] = {&p};
-      CK(hipLaunchKernel(v.fn, dim3(grid), dim3(v.block), args, lds_for(v.wgs), nullptr));
+      CK(hipLaunchKernel(v.fn, dim3((unsigned)(cf.bytes / 16 / v.trip)), dim3(v.block), args, lds_for(v.wgs), nullptr));
     };
     printf("%s\n", cf.name);
     {  // bytes of every variant against the first (production) launch, set 0
