@@ -133,6 +133,33 @@ int main(int argc, char** argv) {
                      var<D2, OP, K2, P, false, 4, 1024>("U4 B1024", 1), var<D2, OP, K2, P, false, 4, 512>("U4 B512", 2),
                      var<D2, OP, K2, P, false, 8, 256>("U8 B256", 0), var<D2, OP, K2, P, false, 8, 256>("U8 B256", 4)}});
   }
+  if (group == "c4pol") {  // C4's 64 MiB buffers (320 MiB streamed) under the nt-store policy too
+    {
+      constexpr int D = nexrInt8, OP = nexrDevMinMax, K = 4;
+      cfgs.push_back({"C4 int8 max K=4 64 MiB: nt loads (production) vs nt loads + stores", K, 64u << 20, all,
+                      {var<D, OP, K, kPolNtLoad, false, 2, 512>("nt-ld U2 B512", 0, 0x7f),
+                       var<D, OP, K, kPolNt, false, 2, 512>("nt-st U2 B512", 0, 0x7f),
+                       var<D, OP, K, kPolNt, false, 1, 1024>("nt-st U1 B1024", 1, 0x7f),
+                       var<D, OP, K, kPolNt, false, 1, 512>("nt-st U1 B512", 2, 0x7f),
+                       var<D, OP, K, kPolNt, false, 4, 256>("nt-st U4 B256", 0, 0x7f),
+                       var<D, OP, K, kPolPlain, false, 2, 512>("plain U2 B512", 0, 0x7f)}});
+    }
+    {
+      constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4;
+      cfgs.push_back({"C4 int32 min K=4 64 MiB: nt loads (production) vs nt loads + stores", K, 64u << 20, all,
+                      {var<D, OP, K, kPolNtLoad, true, 2, 512>("nt-ld U2 B512", 0, 0x80000000ull),
+                       var<D, OP, K, kPolNt, true, 2, 512>("nt-st U2 B512", 0, 0x80000000ull),
+                       var<D, OP, K, kPolNt, true, 1, 1024>("nt-st U1 B1024", 1, 0x80000000ull),
+                       var<D, OP, K, kPolNt, true, 1, 512>("nt-st U1 B512", 2, 0x80000000ull)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 2;
+      cfgs.push_back({"fp32 sum K=2 64 MiB (192 MiB streamed): plain vs nt loads vs nt loads + stores", K, 64u << 20, fin,
+                      {var<D, OP, K, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, K, kPolNt, false, 4, 256>("nt-st U4 B256", 0),
+                       var<D, OP, K, kPolPlain, false, 4, 256>("plain U4 B256", 0)}});
+    }
+  }
   if (group == "k8lanes") {  // lanes per CU at K >= 6: one workgroup of B lanes (U = 1) per CU
     {
       constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8, P = kPolNt;
