@@ -125,11 +125,17 @@ void llSemantics(int* dt, int* op, int* srcIsInput, int* postOp, int* firstWins)
 // there too), non-temporal loads above it, non-temporal loads and stores above
 // NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3) overrides it for
 // sweeps. The workgroup geometry follows the policy (unroll_for/block_for, nexr_internal.h).
-int pickPolicy(uint64_t streamBytes) {
+// One exception (round 5): a two-source, one-destination call takes nt stores as well from
+// NEXR_NT_STORE_K2_MIN_BYTES (96 MiB streamed): 2.2-3.4 % faster at 96-384 MiB, where K = 3 and K = 8
+// are not (tools/occupancy_ab.hip ntstore, profiles/r05q_occupancy_ntstore.txt). nDsts = 0: unknown
+// (a batch), the general rule.
+int pickPolicy(uint64_t streamBytes, int nSrcs = 0, int nDsts = 0) {
   static const long polOverride = envLong("NEXR_POLICY", -1);
   static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);
   static const long ntStoreMin = envLong("NEXR_NT_STORE_MIN_BYTES", 512l << 20);
+  static const long ntStoreK2Min = envLong("NEXR_NT_STORE_K2_MIN_BYTES", 96l << 20);
   if (polOverride >= 0) return polOverride == 0 ? 0 : (polOverride == 1 ? 1 : 3);
+  if (nSrcs == 2 && nDsts == 1 && streamBytes >= (uint64_t)ntStoreK2Min) return 3;
   return streamBytes >= (uint64_t)ntStoreMin ? 3 : (streamBytes >= (uint64_t)ntLoadMin ? 1 : 0);
 }
 
@@ -368,7 +374,7 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   RCParams p;
   fillParams(p, c.nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, c.nPreOp, preOpArgs, c.prePtr, c.postOp);
   Geometry g;
-  const int pol = pickPolicy((uint64_t)(c.nSrcs + nDsts) * nElts * esz);
+  const int pol = pickPolicy((uint64_t)(c.nSrcs + nDsts) * nElts * esz, c.nSrcs, nDsts);
   uint64_t wgs = workgroupsFor(p, c.nSrcs, c.dt, pol);
   if (maxGrid > 0 && wgs > maxGrid) wgs = maxGrid;
   r = pickGeometry(wgs, pol, block_for(c.dt, c.nSrcs, pol), &g);
@@ -967,7 +973,7 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
   RCParams p;
   fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, 0, 0, nullptr, nullptr, 0);
   Geometry g;
-  const int pol = pickPolicy((uint64_t)(nSrcs + nDsts) * nElts * esz);
+  const int pol = pickPolicy((uint64_t)(nSrcs + nDsts) * nElts * esz, nSrcs, nDsts);
   const int block = block_for(datatype, nSrcs, pol);
   r = pickGeometry(workgroupsFor(p, nSrcs, datatype, pol), pol, block, &g);
   if (r != nexrSuccess) return r;

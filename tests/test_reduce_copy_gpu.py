@@ -8,6 +8,7 @@ misalignment, in-place, K=M=8, empty calls).
 """
 import ctypes
 import hashlib
+import os
 import threading
 
 import numpy as np
@@ -193,6 +194,18 @@ def test_hip_graph_capture_and_replay(nexr, oracle, dev):
         for x, y in zip(small_in, small_out):
             xn = x.cpu().numpy()
             assert same(mg.F32, y.cpu().numpy(), oracle.reduce_copy([xn, xn], 1, mg.F32, mg.SUM)[0]), rep
+
+
+def test_first_one_workgroup_per_cu_launch_inside_graph_capture():
+    """The first launch of a kernel that reserves LDS for one workgroup per CU sets the kernel's
+    dynamic-LDS attribute (once per device); in a fresh process that first launch is captured into a
+    HIP graph, and the replays are exact (tests/graph_lds_worker.py)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = subprocess.run([sys.executable, os.path.join(here, "graph_lds_worker.py")], capture_output=True, text=True,
+                       timeout=180)
+    assert p.returncode == 0 and "graph replays exact" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
 
 
 def test_concurrent_callers_on_separate_streams(nexr, oracle, dev):

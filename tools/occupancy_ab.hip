@@ -160,6 +160,32 @@ int main(int argc, char** argv) {
                        var<D, OP, K, kPolPlain, false, 4, 256>("plain U4 B256", 0)}});
     }
   }
+  if (group == "ntstore") {  // where the nt-store policy starts to pay, by fan-in and size
+    constexpr int D = nexrFloat32, OP = nexrDevSum;
+    for (int mib : {16, 32, 64, 128}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=2 %d MiB (%d MiB streamed)", mib, 3 * mib);
+      cfgs.push_back({name, 2, (size_t)mib << 20, fin,
+                      {var<D, OP, 2, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, 2, kPolNt, false, 4, 256>("nt-st U4 B256", 0),
+                       var<D, OP, 2, kPolPlain, false, 4, 256>("plain U4 B256", 0)}});
+    }
+    for (int mib : {16, 48}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=8 %d MiB (%d MiB streamed)", mib, 9 * mib);
+      cfgs.push_back({name, 8, (size_t)mib << 20, fin,
+                      {var<D, OP, 8, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, 8, kPolNt, false, 1, 512>("nt-st U1 B512", 1),
+                       var<D, OP, 8, kPolNtLoad, false, 1, 512>("nt-ld U1 B512", 1)}});
+    }
+    {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=3 64 MiB (256 MiB streamed)");
+      cfgs.push_back({name, 3, 64u << 20, fin,
+                      {var<D, OP, 3, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, 3, kPolNt, false, 4, 256>("nt-st U4 B256", 0)}});
+    }
+  }
   if (group == "k8lanes") {  // lanes per CU at K >= 6: one workgroup of B lanes (U = 1) per CU
     {
       constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8, P = kPolNt;
