@@ -122,10 +122,12 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 // (round-1 steady-state sweeps over U in {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8:
 // profiles/r01_tune_*.log, r01_skew.log, r01s2_geom_*.log). The exceptions, each measured in one process
 // against the alternatives on several boxes with byte-identical outputs:
-//   - K = 4 with non-temporal loads and cached stores (64-512 MiB streamed, C4's regime): U = 2,
-//     B = 512 — +0.9 % on average over 9 datatypes x {sum, min} on four boxes, never below -0.7 %
-//     (profiles/r02_geom_sweep_*.log); at one or two workgroups per CU 1-18 % slower
-//     (profiles/r05l_occupancy_k8lanes.txt);
+//   - K = 4 with non-temporal loads and cached stores (64-512 MiB streamed, C4's regime), 1-, 2- and
+//     8-byte types: U = 2, B = 512 — +0.9 % on average over 9 datatypes x {sum, min} on four boxes in
+//     round 2 (profiles/r02_geom_sweep_*.log); with the round-5 body +0.9-3.6 % for int8, fp16 and bf16,
+//     equal for uint64, and at one or two workgroups per CU 1-18 % slower; 4-byte types keep 4 x 256,
+//     0.7-3.0 % faster with the round-5 body (int32 min at 16-100 MiB, int32 prod, fp32 sum;
+//     profiles/r05s_occupancy_c4sizes.txt, r05t_occupancy_c4types.txt, r05l_occupancy_k8lanes.txt);
 //   - the nt-store policy (>= 512 MiB streamed), where a CU's loads in flight are the lever (round 5,
 //     tools/occupancy_ab.hip, profiles/r05b_occupancy_ab.txt, r05i_occupancy_wide.txt,
 //     r05k_occupancy_k8shape.txt, r05l_occupancy_k8lanes.txt): the fastest point is about 64 KiB of
@@ -148,9 +150,10 @@ struct Shape {
 };
 __host__ __device__ constexpr Shape shape_for(int dt, int k, int pol) {
   const bool half = dt == nexrFloat16 || dt == nexrBfloat16;
+  const bool four = dt == nexrInt32 || dt == nexrUint32 || dt == nexrFloat32;
   return (pol == 3 && k >= 6)                       ? Shape{1, dt == nexrBfloat16 ? 1024 : 512, true}
          : (half && k >= 8)                         ? Shape{1, 1024, true}
-         : (k == 4 && pol == 1)                     ? Shape{2, 512, false}
+         : (k == 4 && pol == 1 && !four)            ? Shape{2, 512, false}
          : (k == 4 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}
                                                     : Shape{4, 256, false};
 }

@@ -77,7 +77,7 @@ MIB = 1 << 20
 
 
 @pytest.mark.parametrize("dt,op,name,buf_mib", [
-    (mg.I8, mg.MINMAX, "min", 16), (mg.I32, mg.PROD, "prod", 16), (mg.F32, mg.SUM, "sum", 13),  # 2 x 512
+    (mg.I8, mg.MINMAX, "min", 16), (mg.I32, mg.PROD, "prod", 16), (mg.F32, mg.SUM, "sum", 13),  # 2 x 512 / 4 x 256
     (mg.U32, mg.MINMAX, "max", 104), (mg.BF16, mg.SUM, "sum", 104),                              # 1 x 1024
     (mg.F16, mg.SUM, "sum", 104)])                                                               # 4 x 256
 def test_k4_policy_geometries_edges(nexr, oracle, dev, dt, op, name, buf_mib):
@@ -90,7 +90,10 @@ def test_k4_policy_geometries_edges(nexr, oracle, dev, dt, op, name, buf_mib):
         info = nexr.query_launch([0x100000 * (i + 1) + (offs[i] if offs else 0) for i in range(4)],
                                  [0x900000 + (offs[4] if offs else 0)], n, dt)
         if offs is None or len(set(offs)) == 1:
-            assert info.generic == 0 and info.block == (512 if info.policy == 1 else 256 if dt == mg.F16 else 1024)
+            if info.policy == 1:
+                assert info.generic == 0 and info.block == (256 if esz == 4 else 512)
+            else:
+                assert info.generic == 0 and info.block == (256 if dt == mg.F16 else 1024)
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
         got = _run(nexr, srcs, dt, op, arg, offs)
         assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)

@@ -186,6 +186,34 @@ int main(int argc, char** argv) {
                        var<D, OP, 3, kPolNt, false, 4, 256>("nt-st U4 B256", 0)}});
     }
   }
+  if (group == "c4sizes") {  // C4's shape by buffer size: is 64 MiB short enough to pay a ramp / tail?
+    constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4;
+    for (int mib : {16, 32, 64, 96, 100}) {
+      char* name = new char[96];
+      snprintf(name, 96, "int32 min K=4 %d MiB (%d MiB streamed)", mib, 5 * mib);
+      cfgs.push_back({name, K, (size_t)mib << 20, all,
+                      {var<D, OP, K, kPolNtLoad, true, 2, 512>("nt-ld U2 B512", 0, 0x80000000ull),
+                       var<D, OP, K, kPolNtLoad, true, 4, 256>("nt-ld U4 B256", 0, 0x80000000ull),
+                       var<D, OP, K, kPolNt, true, 1, 1024>("nt-st U1 B1024", 1, 0x80000000ull)}});
+    }
+  }
+  if (group == "c4types") {  // K = 4 under nt loads (C4's regime), 64 MiB: 2 x 512 against 4 x 256, by type
+    constexpr int K = 4, P = kPolNtLoad;
+#define C4T(D, OP, ISMIN, ARG, NAME, MASK)                                                                  \
+  cfgs.push_back({NAME " K=4 64 MiB (nt loads)", K, 64u << 20, MASK,                                        \
+                  {var<D, OP, K, P, ISMIN, 2, 512>("U2 B512", 0, ARG), var<D, OP, K, P, ISMIN, 4, 256>("U4 B256", 0, ARG), \
+                   var<D, OP, K, P, ISMIN, 4, 256>("U4 B256", 4, ARG)}});
+    C4T(nexrInt8, nexrDevMinMax, false, 0x7f, "int8 max", all)
+    C4T(nexrInt8, nexrDevMinMax, true, 0x80, "int8 min", all)
+    C4T(nexrInt8, nexrDevProd, false, 0, "int8 prod", all)
+    C4T(nexrInt32, nexrDevMinMax, true, 0x80000000ull, "int32 min", all)
+    C4T(nexrInt32, nexrDevProd, false, 0, "int32 prod", all)
+    C4T(nexrFloat32, nexrDevSum, false, 0, "fp32 sum", fin)
+    C4T(nexrBfloat16, nexrDevSum, false, 0, "bf16 sum", fin)
+    C4T(nexrFloat16, nexrDevSum, false, 0, "fp16 sum", fin)
+    C4T(nexrUint64, nexrDevSum, false, 0, "uint64 sum", all)
+#undef C4T
+  }
   if (group == "k8lanes") {  // lanes per CU at K >= 6: one workgroup of B lanes (U = 1) per CU
     {
       constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8, P = kPolNt;
