@@ -170,16 +170,23 @@ struct ResPrims {
   ResShared* sh;  // the wait's outcome and the attached steps, broadcast from thread 0
 
   // waitPeer's spin (prims_simple.h:116-123), thread 0 only, bounded like checkAbort
-  // (primitives.h:142-156): false after a timeout (status set) or once another workgroup's timeout
-  // is visible in the status word.
+  // (primitives.h:142-156): false after a timeout (status 1) or once the status word is non-zero:
+  // another workgroup's timeout, or the host's relay of the communicator's abort word (2), which a
+  // workgroup that gives up on it turns into 3, so that the host can tell a kernel that stopped
+  // mid-protocol from one that finished before the relay arrived.
   __device__ __forceinline__ bool wait_ge(const char* p, uint64_t target) const {
     uint64_t t0 = 0;
     for (uint32_t spins = 0;; spins++) {
       if (ctr_ld(p) >= target) return true;
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (!t0) t0 = now;
-      if ((spins & 255) == 255 && __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
-        return false;
+      if ((spins & 255) == 255) {
+        const uint32_t st = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (st != 0) {
+          if (st == 2) __hip_atomic_store(a.status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return false;
+        }
+      }
       if (now - t0 > a.timeoutTicks) {
         __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return false;

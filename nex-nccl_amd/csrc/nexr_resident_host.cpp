@@ -499,7 +499,9 @@ nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* 
       break;
     }
     if (!relayed && ph->abort.load(std::memory_order_acquire)) {
-      __atomic_store_n(c->resStatus[0], 2u, __ATOMIC_RELEASE);
+      // Only over a clean word: a timeout the kernel already reported (1) must stay visible.
+      uint32_t clean = 0;
+      __atomic_compare_exchange_n(c->resStatus[0], &clean, 2u, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
       relayed = true;
     }
     if (std::chrono::steady_clock::now() - pollStart > std::chrono::milliseconds(2))
@@ -508,7 +510,12 @@ nexrResult_t residentPeerAllReduce(nexrRingComm* c, const void* sendbuff, void* 
       std::this_thread::yield();
   }
   if (hipStreamSynchronize(s) != hipSuccess && r == nexrSuccess) r = nexrUnhandledCudaError;
-  if (r == nexrSuccess && __atomic_load_n(c->resStatus[0], __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
+  // 1: a step wait timed out; 3: a workgroup gave up on the relayed abort (mid-protocol either way).
+  // 2 left as relayed: no wait saw it, the kernel ran this rank's whole schedule before the relay
+  // arrived (another rank failed a LATER call, e.g. at the capacity guard above): this call succeeded.
+  const uint32_t st = __atomic_load_n(c->resStatus[0], __ATOMIC_ACQUIRE);
+  if (st == 2) __atomic_store_n(c->resStatus[0], 0u, __ATOMIC_RELEASE);
+  else if (r == nexrSuccess && st != 0) r = nexrInternalError;
   if (r != nexrSuccess) {
     c->broken = true;
     peerHeader(c->shm)->abort.store(1);

@@ -9,6 +9,7 @@ import argparse
 import importlib
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.dirname(HERE), os.path.join(HERE, "golden")]
@@ -24,9 +25,10 @@ def main() -> int:
     for name in ("rank", "n", "dt", "op", "count", "seed", "proto", "buff", "calls"):
         ap.add_argument(f"--{name}", type=int, required=True)
     ap.add_argument("--coll", default="allreduce",
-                    choices=["allreduce", "allreduce_resident", "allreduce_mixed", "reducescatter", "allgather", "reduce", "broadcast",
-                             "sendrecv"])
+                    choices=["allreduce", "allreduce_resident", "allreduce_mixed", "allreduce_guard", "reducescatter",
+                             "allgather", "reduce", "broadcast", "sendrecv"])
     ap.add_argument("--root", type=int, default=0)
+    ap.add_argument("--dt2", type=int, default=-1, help="allreduce_guard: the second call's datatype")
     ap.add_argument("--shm", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -44,12 +46,37 @@ def main() -> int:
     send = torch.from_numpy(inputs[a.rank].copy()).to(dev)
     recv = torch.zeros(n_out, dtype=send.dtype, device=dev)
     torch.cuda.synchronize()
-    resident = a.coll in ("allreduce_resident", "allreduce_mixed")
+    resident = a.coll in ("allreduce_resident", "allreduce_mixed", "allreduce_guard")
     extras = resident or a.coll == "sendrecv"  # the opt-in extras library (include/nexr_extras.h)
     with ring.PeerRingComm(a.n, a.rank, a.shm, device=ordinal, buff_bytes=a.buff, protocol=a.proto,
                            timeout_ms=20000 if resident else 60000, extras=extras) as comm:
         with open(f"{a.out}.device", "w") as f:  # the GPU, the GPU count, and the step wait in effect
             f.write(f"{ordinal} {torch.cuda.device_count()} {comm.step_wait()}\n")
+        if a.coll == "allreduce_guard":
+            # Call 0 agrees the team on its (datatype, op) kernel; call 1 runs a kernel that keeps fewer
+            # workgroups resident per CU. Record how call 1 ended (result code, 0 = success) and how long
+            # it took: a rank must return, not wait for peers whose workgroups cannot be scheduled.
+            comm.all_reduce_resident(send.data_ptr(), recv.data_ptr(), a.count, a.dt, a.op)
+            np.save(f"{a.out}.0.npy", recv.cpu().numpy())
+            # Every rank past call 0 before any starts call 1: a rank failing call 1 aborts the
+            # communicator, and with it any rank still inside call 0.
+            open(f"{a.out}.call0", "w").close()
+            base = os.path.join(os.path.dirname(a.out), "rank")
+            t_end = time.monotonic() + 60
+            while not all(os.path.exists(f"{base}{q}.call0") for q in range(a.n)):
+                assert time.monotonic() < t_end, "ranks did not all finish call 0"
+                time.sleep(0.005)
+            x = torch.from_numpy(mg.gen_inputs(a.dt2, a.n, a.count, a.seed + 1, special=True)[a.rank].copy()).to(dev)
+            torch.cuda.synchronize()
+            t0 = time.monotonic()
+            try:
+                comm.all_reduce_resident(x.data_ptr(), x.data_ptr(), a.count, a.dt2, a.op)
+                code = 0
+            except Exception as e:  # NexrError carries the ncclResult_t value
+                code = getattr(e, "code", -1)
+            with open(f"{a.out}.guard", "w") as f:
+                f.write(f"{code} {time.monotonic() - t0:.3f}\n")
+            return 0
         if a.coll not in ("allreduce", "allreduce_resident", "allreduce_mixed"):
             for call in range(a.calls):
                 if a.coll == "reducescatter":

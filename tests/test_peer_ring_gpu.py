@@ -29,7 +29,7 @@ def ring_extras_available() -> bool:
     return importlib.import_module("nex-nccl_amd.ring").extras_available()
 
 
-def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="allreduce", root=0):
+def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="allreduce", root=0, extra=(), env=None):
     name = f"/nexr_test_{uuid.uuid4().hex[:16]}"
     out = [str(tmp_path / f"rank{r}") for r in range(n)]
     procs = []
@@ -37,8 +37,9 @@ def _run_ring(tmp_path, n, dt, op, count, proto, buff, calls=2, seed=7, coll="al
         for r in range(n):
             cmd = [sys.executable, WORKER, "--rank", str(r), "--n", str(n), "--dt", str(dt), "--op", str(op),
                    "--count", str(count), "--seed", str(seed), "--proto", str(proto), "--buff", str(buff),
-                   "--calls", str(calls), "--shm", name, "--out", out[r], "--coll", coll, "--root", str(root)]
-            procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+                   "--calls", str(calls), "--shm", name, "--out", out[r], "--coll", coll, "--root", str(root), *extra]
+            procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                          env=None if env is None else dict(os.environ, **env)))
         logs = []
         for p in procs:
             try:
@@ -107,6 +108,37 @@ def test_peer_ring_resident_processes(oracle, tmp_path, n, dt, op):
     for r in range(n):
         assert mg.canon_bytes(dt, outs[r][0]) == mg.canon_bytes(dt, exp0[r]), f"rank {r}, call 0"
         assert mg.canon_bytes(dt, outs[r][1]) == mg.canon_bytes(dt, exp1[r]), f"rank {r}, call 1 (in place)"
+
+
+def test_peer_ring_resident_guard_fails_every_rank_fast(oracle, tmp_path):
+    """The process ranks agree their team on the first call's kernel (residentPeerTeam); a later call
+    whose (datatype, op) kernel keeps fewer workgroups resident per CU must not launch a grid that
+    cannot be resident beside the other ranks' grids (nexr_resident_host.cpp, the per-call capacity
+    guard in residentPeerAllReduce). Nine ranks on one GPU with NEXR_RESIDENT_TEAM=128: the fp32 sum
+    kernel (58 VGPRs, 7 workgroups per CU: 1,792 on 256 CUs) agrees 128 workgroups per rank, 1,152 in
+    all; the bf16 sum kernel (99 VGPRs, 4 per CU: 1,024) cannot hold them. Every rank must return
+    from the second call within seconds with InvalidUsage (its own guard) or RemoteError /
+    InternalError (the shared abort word raised by another rank), and none may hang. Ranks spread over
+    several GPUs share each GPU with fewer ranks, so the guard need not fire: one GPU only."""
+    if not ring_extras_available():
+        pytest.skip("libnexr_extras.so not built (opt-in: make -C nex-nccl_amd/csrc EXTRAS=1)")
+    if torch.cuda.device_count() != 1:
+        pytest.skip("the capacity arithmetic assumes every rank on one GPU")
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("the capacity arithmetic assumes 256 CUs (MI355X)")
+    from oracle.ring import ring_allreduce_expected
+    n, count, buff = 9, 100_003, 1 << 18
+    outs = _run_ring(tmp_path, n, mg.F32, 0, count, 0, buff, calls=1, coll="allreduce_guard",
+                     extra=("--dt2", str(mg.BF16)), env={"NEXR_RESIDENT_TEAM": "128"})
+    exp = ring_allreduce_expected(mg.gen_inputs(mg.F32, n, count, 7, special=True), mg.F32, 0, buff)
+    codes = []
+    for r in range(n):
+        assert mg.canon_bytes(mg.F32, outs[r][0]) == mg.canon_bytes(mg.F32, exp[r]), f"rank {r}, first call"
+        code, secs = open(tmp_path / f"rank{r}.guard").read().split()
+        codes.append(int(code))
+        assert float(secs) < 10.0, f"rank {r} took {secs} s to fail"
+    assert all(c in (3, 5, 6) for c in codes), codes  # InternalError, InvalidUsage, RemoteError
+    assert 5 in codes, codes
 
 
 @pytest.mark.parametrize("n,dt,op", [(2, mg.F32, 0), (3, mg.I32, 0)])
