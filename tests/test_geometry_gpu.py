@@ -180,3 +180,46 @@ def test_16bit_wide_fan_in_nt_store_geometry(nexr, oracle, dev, dt, k):
     assert (info.policy, info.block, info.packsPerLane) == (3, 512 if dt == mg.F16 else 1024, 1)
     exp = oracle.reduce_copy(srcs, 1, dt, mg.SUM, 0, threads=16)[0]
     assert mg.canon_bytes(dt, _run(nexr, srcs, dt, mg.SUM, 0)) == mg.canon_bytes(dt, exp)
+
+
+# ---- K <= 2 with M <= 2: nt stores from 96 MiB streamed (round 5, nexr_api.cpp pickPolicy) ---------------
+def _run_m(nexr, srcs, m, dt, op, arg, offs):
+    n, esz = srcs[0].size, srcs[0].itemsize
+    bufs = []
+    for s, o in zip(srcs, offs):
+        b = torch.zeros(n * esz + o + 64, dtype=torch.uint8, device="cuda")
+        b[o:o + n * esz] = torch.from_numpy(s.view(np.uint8).copy()).cuda()
+        bufs.append(b)
+    douts = offs[len(srcs):]
+    outs = [torch.full((n * esz + o + 64,), 0x5A, dtype=torch.uint8, device="cuda") for o in douts]
+    nexr.reduce_copy_ptrs([b.data_ptr() + o for b, o in zip(bufs, offs)], [t.data_ptr() + o for t, o in zip(outs, douts)],
+                          n, dt, op, arg, None, False, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = []
+    for t, o in zip(outs, douts):
+        host = t.cpu().numpy()
+        assert (host[:o] == 0x5A).all() and (host[o + n * esz:] == 0x5A).all(), "write outside a destination"
+        got.append(host[o:o + n * esz].view(srcs[0].dtype))
+    return got
+
+
+@pytest.mark.parametrize("dt,k,m,op,name,buf_mib", [(mg.F32, 1, 1, mg.SUM, "sum", 49), (mg.I8, 1, 2, mg.MINMAX, "max", 33),
+                                                    (mg.F32, 2, 2, mg.SUM, "sum", 25), (mg.BF16, 2, 2, mg.PROD, "prod", 26)])
+def test_small_fan_in_nt_store_policy_edges(nexr, oracle, dev, dt, k, m, op, name, buf_mib):
+    """Copies (K = 1) and the ring's two-destination steps just past 96 MiB streamed launch the nt-store
+    policy at the default 4 x 256 shape; whole trips, a remainder plus edges, and mixed 16-B phases
+    against the oracle bit for bit, every destination, guard bytes intact."""
+    esz = np.dtype(mg.STORE[dt]).itemsize
+    base = buf_mib * MIB // esz
+    arg = mg.minmax_arg(dt, name == "max") if op == mg.MINMAX else 0
+    mixed = [(i * 3) % 16 // esz * esz for i in range(k + m)]
+    for n, offs in ((base, [0] * (k + m)), (base + 16 // esz * 1024 * 3 + 5, [esz] * (k + m)), (base - 7, mixed)):
+        info = nexr.query_launch([0x1000000 * (i + 1) + offs[i] for i in range(k)],
+                                 [0x90000000 + 0x1000000 * d + offs[k + d] for d in range(m)], n, dt)
+        assert (info.policy, info.block, info.packsPerLane) == (3, 256, 4), (n, offs)
+        srcs = mg.gen_inputs(dt, k, n, 5100 + n % 1009, special=True)
+        exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
+        for got in _run_m(nexr, srcs, m, dt, op, arg, offs):
+            assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)
+        del srcs, exp
+        torch.cuda.empty_cache()

@@ -63,6 +63,7 @@ struct Cfg {
   size_t bytes;
   uint32_t mask;
   std::vector<Var> vars;
+  int m = 1;  // destinations (all written; the byte check reads the first)
 };
 
 template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
@@ -184,6 +185,25 @@ int main(int argc, char** argv) {
       cfgs.push_back({name, 3, 64u << 20, fin,
                       {var<D, OP, 3, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
                        var<D, OP, 3, kPolNt, false, 4, 256>("nt-st U4 B256", 0)}});
+    }
+  }
+  if (group == "ntstore2") {  // the policy edge for K = 1 copies and K = 2, M = 2 ring steps (96-512 MiB streamed)
+    constexpr int D = nexrFloat32, OP = nexrDevSum;
+    for (int mib : {32, 48, 64, 128, 192, 255}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 copy K=1 M=1 %d MiB (%d MiB streamed)", mib, 2 * mib);
+      cfgs.push_back({name, 1, (size_t)mib << 20, fin,
+                      {var<D, OP, 1, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, 1, kPolNt, false, 4, 256>("nt-st U4 B256", 0),
+                       var<D, OP, 1, kPolPlain, false, 4, 256>("plain U4 B256", 0)}});
+    }
+    for (int mib : {16, 24, 32, 64, 96, 127}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=2 M=2 %d MiB (%d MiB streamed)", mib, 4 * mib);
+      cfgs.push_back({name, 2, (size_t)mib << 20, fin,
+                      {var<D, OP, 2, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, 2, kPolNt, false, 4, 256>("nt-st U4 B256", 0),
+                       var<D, OP, 2, kPolPlain, false, 4, 256>("plain U4 B256", 0)}, 2});
     }
   }
   if (group == "c4sizes") {  // C4's shape by buffer size: is 64 MiB short enough to pay a ramp / tail?
@@ -314,9 +334,11 @@ int main(int argc, char** argv) {
         p.src[s] = q;
         owned.push_back(q);
       }
-      CK(hipMalloc((void**)&p.dst[0], cf.bytes));
-      owned.push_back(p.dst[0]);
-      p.nDsts = 1;
+      for (int d = 0; d < cf.m; d++) {
+        CK(hipMalloc((void**)&p.dst[d], cf.bytes));
+        owned.push_back(p.dst[d]);
+      }
+      p.nDsts = cf.m;
       p.nPacks = cf.bytes / 16;
       p.head = 0;
     }
@@ -332,7 +354,8 @@ int main(int argc, char** argv) {
     };
     for (const Var& v : cf.vars) {
       const RCParams p = params(v, 0);
-      if (p.nElts * (uint64_t)v.esz != p.nPacks * 16 || p.nPacks % kTripPacks != 0 || cf.k > NEXR_MAX_SRCS) {
+      if (p.nElts * (uint64_t)v.esz != p.nPacks * 16 || p.nPacks % kTripPacks != 0 || cf.k > NEXR_MAX_SRCS ||
+          cf.m < 1 || cf.m > NEXR_MAX_DSTS) {
         fprintf(stderr, "bad parameters for %s / %s\n", cf.name, v.name.c_str());
         return 2;
       }
@@ -371,7 +394,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         us[vi].push_back(ms * 1e3f / BLK);
       }
-    const double alg = (double)(cf.k + 1) * cf.bytes;
+    const double alg = (double)(cf.k + cf.m) * cf.bytes;
     double med0 = 0;
     for (size_t vi = 0; vi < cf.vars.size(); vi++) {
       std::vector<float> s = us[vi];
