@@ -206,6 +206,23 @@ int main(int argc, char** argv) {
                        var<D, OP, 2, kPolPlain, false, 4, 256>("plain U4 B256", 0)}, 2});
     }
   }
+  if (group == "ntstore3") {  // the tree schedule's other shapes: K = 1 with M = 3-4, K = 3-4 with M = 2
+    constexpr int D = nexrFloat32, OP = nexrDevSum;
+    struct KM { int k, m, mib; };
+    for (KM c : {KM{1, 3, 24}, KM{1, 3, 64}, KM{1, 4, 20}, KM{1, 4, 60}, KM{3, 2, 20}, KM{3, 2, 60},
+                 KM{3, 1, 32}, KM{4, 2, 16}, KM{4, 2, 48}}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=%d M=%d %d MiB (%d MiB streamed)", c.k, c.m, c.mib, (c.k + c.m) * c.mib);
+      std::vector<Var> v;
+#define NT3(K)                                                                                           \
+  v = {var<D, OP, K, kPolNtLoad, false, unroll_for(D, K, kPolNtLoad), block_for(D, K, kPolNtLoad)>("nt-ld", 0), \
+       var<D, OP, K, kPolNt, false, unroll_for(D, K, kPolNt), block_for(D, K, kPolNt)>("nt-st", lds_for(D, K, kPolNt) ? 1 : 0), \
+       var<D, OP, K, kPolPlain, false, 4, 256>("plain", 0)};
+      if (c.k == 1) { NT3(1) } else if (c.k == 3) { NT3(3) } else { NT3(4) }
+#undef NT3
+      cfgs.push_back({name, c.k, (size_t)c.mib << 20, fin, v, c.m});
+    }
+  }
   if (group == "c4sizes") {  // C4's shape by buffer size: is 64 MiB short enough to pay a ramp / tail?
     constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4;
     for (int mib : {16, 32, 64, 96, 100}) {
