@@ -223,6 +223,29 @@ int main(int argc, char** argv) {
       cfgs.push_back({name, c.k, (size_t)c.mib << 20, fin, v, c.m});
     }
   }
+  if (group == "c3pol") {  // C3 (K = 8, 256 MiB per buffer, 2.25 GiB streamed) and C2: nt stores or nt loads only
+    {
+      constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8;
+      cfgs.push_back({"C3 fp16 sum K=8 256 MiB: nt loads + stores (production) vs nt loads only", K, 256u << 20, fin,
+                      {var<D, OP, K, kPolNt, false, 1, 512>("nt-st U1 B512", 1), var<D, OP, K, kPolNtLoad, false, 1, 512>("nt-ld U1 B512", 1),
+                       var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 1),
+                       var<D, OP, K, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0)}});
+    }
+    {
+      constexpr int D = nexrBfloat16, OP = nexrDevSum, K = 8;
+      cfgs.push_back({"C3 bf16 sum K=8 256 MiB: nt loads + stores (production) vs nt loads only", K, 256u << 20, fin,
+                      {var<D, OP, K, kPolNt, false, 1, 1024>("nt-st U1 B1024", 1),
+                       var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 1),
+                       var<D, OP, K, kPolNtLoad, false, 1, 512>("nt-ld U1 B512", 1)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K = 2;
+      cfgs.push_back({"C2 fp32 sum K=2 256 MiB: nt loads + stores (production) vs nt loads only vs plain", K, 256u << 20, fin,
+                      {var<D, OP, K, kPolNt, false, 4, 256>("nt-st U4 B256", 0),
+                       var<D, OP, K, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, K, kPolPlain, false, 4, 256>("plain U4 B256", 0)}});
+    }
+  }
   if (group == "c4sizes") {  // C4's shape by buffer size: is 64 MiB short enough to pay a ramp / tail?
     constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4;
     for (int mib : {16, 32, 64, 96, 100}) {
