@@ -56,6 +56,7 @@ struct Var {
   int esz;
   int trip;  // packs per workgroup trip (U x B)
   uint64_t redArg;
+  int k;  // the fan-in the kernel was compiled for: must equal the configuration's source count
 };
 struct Cfg {
   const char* name;
@@ -70,7 +71,7 @@ template <int D, int OP, int K, int POL, bool IsMin, int U, int B>
 Var var(const char* geom, int wgs, uint64_t redArg = 0) {
   char buf[128];
   snprintf(buf, sizeof buf, "%s, %d WG/CU%s", geom, wgs > 0 ? wgs : 0, wgs > 0 ? "" : " (registers)");
-  return Var{buf, (const void*)&reduce_copy_kernel<D, OP, K, POL, IsMin, U, B>, B, wgs, 16 / Ty<D>::EPP, U * B, redArg};
+  return Var{buf, (const void*)&reduce_copy_kernel<D, OP, K, POL, IsMin, U, B>, B, wgs, 16 / Ty<D>::EPP, U * B, redArg, K};
 }
 
 int main(int argc, char** argv) {
@@ -209,8 +210,12 @@ int main(int argc, char** argv) {
   if (group == "ntstore3") {  // the tree schedule's other shapes: K = 1 with M = 3-4, K = 3-4 with M = 2
     constexpr int D = nexrFloat32, OP = nexrDevSum;
     struct KM { int k, m, mib; };
-    for (KM c : {KM{1, 3, 24}, KM{1, 3, 64}, KM{1, 4, 20}, KM{1, 4, 60}, KM{3, 2, 20}, KM{3, 2, 60},
-                 KM{3, 1, 32}, KM{4, 2, 16}, KM{4, 2, 48}}) {
+    const bool wideM = argc > 3 && std::string(argv[3]) == "m5";  // M = 5-8 (ntstore3 m5)
+    const std::vector<KM> shapes = wideM ? std::vector<KM>{KM{1, 5, 16}, KM{1, 5, 48}, KM{1, 8, 12}, KM{1, 8, 32},
+                                                           KM{2, 6, 12}, KM{2, 6, 36}, KM{3, 5, 12}, KM{3, 5, 32}}
+                                         : std::vector<KM>{KM{1, 3, 24}, KM{1, 3, 64}, KM{1, 4, 20}, KM{1, 4, 60}, KM{3, 2, 20},
+                                                           KM{3, 2, 60}, KM{3, 1, 32}, KM{4, 2, 16}, KM{4, 2, 48}};
+    for (KM c : shapes) {
       char* name = new char[96];
       snprintf(name, 96, "fp32 sum K=%d M=%d %d MiB (%d MiB streamed)", c.k, c.m, c.mib, (c.k + c.m) * c.mib);
       std::vector<Var> v;
@@ -218,7 +223,7 @@ int main(int argc, char** argv) {
   v = {var<D, OP, K, kPolNtLoad, false, unroll_for(D, K, kPolNtLoad), block_for(D, K, kPolNtLoad)>("nt-ld", 0), \
        var<D, OP, K, kPolNt, false, unroll_for(D, K, kPolNt), block_for(D, K, kPolNt)>("nt-st", lds_for(D, K, kPolNt) ? 1 : 0), \
        var<D, OP, K, kPolPlain, false, 4, 256>("plain", 0)};
-      if (c.k == 1) { NT3(1) } else if (c.k == 3) { NT3(3) } else { NT3(4) }
+      if (c.k == 1) { NT3(1) } else if (c.k == 2) { NT3(2) } else if (c.k == 3) { NT3(3) } else { NT3(4) }
 #undef NT3
       cfgs.push_back({name, c.k, (size_t)c.mib << 20, fin, v, c.m});
     }
@@ -395,7 +400,7 @@ int main(int argc, char** argv) {
     for (const Var& v : cf.vars) {
       const RCParams p = params(v, 0);
       if (p.nElts * (uint64_t)v.esz != p.nPacks * 16 || p.nPacks % kTripPacks != 0 || cf.k > NEXR_MAX_SRCS ||
-          cf.m < 1 || cf.m > NEXR_MAX_DSTS) {
+          cf.m < 1 || cf.m > NEXR_MAX_DSTS || v.k != cf.k) {
         fprintf(stderr, "bad parameters for %s / %s\n", cf.name, v.name.c_str());
         return 2;
       }
