@@ -126,20 +126,20 @@ void llSemantics(int* dt, int* op, int* srcIsInput, int* postOp, int* firstWins)
 // NEXR_NT_STORE_MIN_BYTES (512 MiB = 2x the Infinity Cache). NEXR_POLICY (0/1/3) overrides it for
 // sweeps. The workgroup geometry follows the policy (unroll_for/block_for, nexr_internal.h).
 // One exception (round 5): calls with few sources take nt stores as well from
-// NEXR_NT_STORE_K2_MIN_BYTES (96 MiB streamed) — K <= 2 with M <= 4, and K = 3 with M = 2-4 — where
-// K = 3 with one destination is mixed and K = 4 and K = 8 lose (tools/occupancy_ab.hip ntstore /
-// ntstore2 / ntstore3 / c4pol): K = 2 M = 1 2.2-3.4 % faster at 96-384 MiB
-// (profiles/r05q_occupancy_ntstore.txt), K = 1 copies 1.9-4.8 % at 96-510 MiB, the ring's K = 2 M = 2
-// steps 2.5-6.3 % at 96-508 MiB (profiles/r05zd_occupancy_ntstore2.txt), the tree's K = 1 M = 3-4 and
-// K = 3 M = 2 steps 1.1-3.4 % at 96-300 MiB (profiles/r05zg_occupancy_ntstore3.txt). M >= 5 was not
-// measured. nDsts = 0: unknown (a batch), the general rule.
+// NEXR_NT_STORE_K2_MIN_BYTES (96 MiB streamed), for the (K, M) measured to gain at 96-510 MiB
+// (tools/occupancy_ab.hip ntstore / ntstore2 / ntstore3 / c4pol): K = 1 with M = 1-4 (1.1-4.8 %),
+// K = 2 with M = 1-6 (2.2-6.3 %), K = 3 with M = 2-5 (3.1-5.6 %) (profiles/r05q_occupancy_ntstore.txt,
+// r05zd_occupancy_ntstore2.txt, r05zg_occupancy_ntstore3.txt, r05zj_occupancy_ntstore3_m5.txt). Outside
+// it nt stores were mixed (K = 3 M = 1, K = 1 M = 5) or lost (K = 1 M = 8: 2.9-5.9 %, K = 4 M = 2,
+// K = 8). nDsts = 0: unknown (a batch), the general rule.
+constexpr int kNtStoreMinM[4] = {0, 1, 1, 2}, kNtStoreMaxM[4] = {0, 4, 6, 5};
 int pickPolicy(uint64_t streamBytes, int nSrcs = 0, int nDsts = 0) {
   static const long polOverride = envLong("NEXR_POLICY", -1);
   static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);
   static const long ntStoreMin = envLong("NEXR_NT_STORE_MIN_BYTES", 512l << 20);
   static const long ntStoreK2Min = envLong("NEXR_NT_STORE_K2_MIN_BYTES", 96l << 20);
   if (polOverride >= 0) return polOverride == 0 ? 0 : (polOverride == 1 ? 1 : 3);
-  const bool fewSrcs = (nSrcs >= 1 && nSrcs <= 2 && nDsts >= 1 && nDsts <= 4) || (nSrcs == 3 && nDsts >= 2 && nDsts <= 4);
+  const bool fewSrcs = nSrcs >= 1 && nSrcs <= 3 && nDsts >= kNtStoreMinM[nSrcs] && nDsts <= kNtStoreMaxM[nSrcs];
   if (fewSrcs && streamBytes >= (uint64_t)ntStoreK2Min) return 3;
   return streamBytes >= (uint64_t)ntStoreMin ? 3 : (streamBytes >= (uint64_t)ntLoadMin ? 1 : 0);
 }
