@@ -262,6 +262,24 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     assert nexr.query_launch([0x1000], [0x3000], 0, 7).grid == 0
 
 
+def test_nt_store_table_at_its_threshold(nexr):
+    """pickPolicy's (K, M) table (nexr_api.cpp, round 5): every K = 1..8 x M = 1..8 just at and just
+    below 96 MiB streamed. Inside the table (K = 1 with M = 1-4, K = 2 with M = 1-6, K = 3 with M = 2-5)
+    the call takes nt loads + stores (3) from 96 MiB; everywhere else, and below 96 MiB, the general
+    rule's nt loads (1) between 64 and 512 MiB."""
+    table = {1: range(1, 5), 2: range(1, 7), 3: range(2, 6)}
+    mib96 = 96 << 20
+    for k in range(1, 9):
+        for m in range(1, 9):
+            n = -(-mib96 // (k + m))  # the first size streaming >= 96 MiB (uint8: 1 byte per element)
+            srcs = [0x100000000 * (i + 1) for i in range(k)]
+            dsts = [0x1000000000 + 0x100000000 * d for d in range(m)]
+            at = nexr.query_launch(srcs, dsts, n, 1).policy
+            below = nexr.query_launch(srcs, dsts, n - 1, 1).policy
+            assert at == (3 if m in table.get(k, ()) else 1), (k, m)
+            assert below == 1, (k, m)
+
+
 def test_empty_calls_are_noops(nexr):
     # nElts == 0 and nDsts == 0 return success without launching (common_kernel.h:288-289).
     assert _call(nexr, n=0) == 0
