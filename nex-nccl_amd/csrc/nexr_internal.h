@@ -138,9 +138,10 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 //         K = 6 1.3 %; 256 lanes are 10-20 % slower, 384 or 640 lanes 2 % slower;
 //       bf16, K >= 6: U = 1, B = 1024 — its fold is ~15x the VALU of fp16's, and 512 lanes per CU do not
 //         hide it (2.9 % slower than 1024);
-//   - 16-bit floats, K >= 8, below the nt-store policy: U = 1, B = 1024 at one workgroup per CU (rounds 1
-//     and 5: fp16 399.9 vs 407.9 us, bf16 394.9 vs 402.0 us at C3 against 4 x 256,
-//     profiles/r01s3_*_geometry_ab.txt).
+//   - 16-bit floats, K >= 8, below the nt-store policy: U = 1, B = 1024 as the registers admit (two per
+//     CU): rounds 1 and 5 chose 1 x 1024 over 4 x 256 (profiles/r01s3_*_geometry_ab.txt); held to one
+//     workgroup per CU it is 3.2-9.3 % slower under nt loads (64-512 MiB streamed) and equal under plain
+//     (profiles/r05zm_occupancy_k8mid.txt) — the reservation pays only under nt stores (above).
 // K = 2 keeps the default everywhere (U = 1 loses 10-13 %, U = 2 loses 1-5 %; 2 to 8 workgroups per CU
 // are flat, profiles/r05b_occupancy_ab.txt).
 constexpr int kTripPacks = 1024;  // the default trip (4 x 256)
@@ -152,7 +153,7 @@ __host__ __device__ constexpr Shape shape_for(int dt, int k, int pol) {
   const bool half = dt == nexrFloat16 || dt == nexrBfloat16;
   const bool four = dt == nexrInt32 || dt == nexrUint32 || dt == nexrFloat32;
   return (pol == 3 && k >= 6)                       ? Shape{1, dt == nexrBfloat16 ? 1024 : 512, true}
-         : (half && k >= 8)                         ? Shape{1, 1024, true}
+         : (half && k >= 8)                         ? Shape{1, 1024, false}
          : (k == 4 && pol == 1 && !four)            ? Shape{2, 512, false}
          : (k == 4 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}
                                                     : Shape{4, 256, false};

@@ -1,7 +1,8 @@
 """Child process of tests/test_reduce_copy_gpu.py::test_first_one_workgroup_per_cu_launch_inside_graph_capture:
-the process's FIRST launch of a kernel that reserves LDS for one workgroup per CU (fp16 K = 8, where
-the launch also sets the kernel's dynamic-LDS attribute once per device) happens inside a HIP graph
-capture; the graph is replayed on new data and compared with the oracle bit for bit."""
+the process's FIRST launch of a kernel that reserves LDS for one workgroup per CU (fp16 K = 8 under the
+nt-store policy, forced by the parent with NEXR_POLICY=3; the launch also sets the kernel's dynamic-LDS
+attribute once per device) happens inside a HIP graph capture; the graph is replayed on new data and
+compared with the oracle bit for bit. The worker checks the launch shape before capturing."""
 import importlib
 import os
 import sys
@@ -21,6 +22,10 @@ def main() -> int:
     n, k = 1_000_003, 8
     ins = [torch.zeros(n, dtype=torch.float16, device="cuda") for _ in range(k)]
     out = torch.zeros(n, dtype=torch.float16, device="cuda")
+    info = nexr.query_launch([t.data_ptr() for t in ins], [out.data_ptr()], n, mg.F16)
+    if (info.policy, info.block, info.packsPerLane) != (3, 512, 1):
+        print(f"not the one-workgroup-per-CU shape: policy {info.policy} block {info.block}")
+        return 1
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):

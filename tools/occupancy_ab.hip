@@ -251,6 +251,31 @@ int main(int argc, char** argv) {
                        var<D, OP, K, kPolPlain, false, 4, 256>("plain U4 B256", 0)}});
     }
   }
+  if (group == "k8mid") {  // 16-bit K = 8 below the nt-store policy: production 1 x 1024 at one workgroup per CU
+    constexpr int OP = nexrDevSum, K = 8;
+    for (int mib : {4, 16, 48}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp16 sum K=8 %d MiB (%d MiB streamed)", mib, 9 * mib);
+      constexpr int D = nexrFloat16;
+      if (mib == 4)
+        cfgs.push_back({name, K, (size_t)mib << 20, fin,
+                        {var<D, OP, K, kPolPlain, false, 1, 1024>("plain U1 B1024", 1), var<D, OP, K, kPolPlain, false, 4, 256>("plain U4 B256", 0),
+                         var<D, OP, K, kPolPlain, false, 1, 512>("plain U1 B512", 1), var<D, OP, K, kPolPlain, false, 1, 1024>("plain U1 B1024", 0)}});
+      else
+        cfgs.push_back({name, K, (size_t)mib << 20, fin,
+                        {var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 1), var<D, OP, K, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                         var<D, OP, K, kPolNtLoad, false, 1, 512>("nt-ld U1 B512", 1), var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 0),
+                         var<D, OP, K, kPolNt, false, 1, 512>("nt-st U1 B512", 1)}});
+    }
+    for (int mib : {16, 48}) {
+      char* name = new char[96];
+      snprintf(name, 96, "bf16 sum K=8 %d MiB (%d MiB streamed)", mib, 9 * mib);
+      constexpr int D = nexrBfloat16;
+      cfgs.push_back({name, K, (size_t)mib << 20, fin,
+                      {var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 1), var<D, OP, K, kPolNtLoad, false, 4, 256>("nt-ld U4 B256", 0),
+                       var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 0), var<D, OP, K, kPolNt, false, 1, 1024>("nt-st U1 B1024", 1)}});
+    }
+  }
   if (group == "c4sizes") {  // C4's shape by buffer size: is 64 MiB short enough to pay a ramp / tail?
     constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4;
     for (int mib : {16, 32, 64, 96, 100}) {
