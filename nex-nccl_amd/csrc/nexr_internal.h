@@ -132,8 +132,12 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 //     tools/occupancy_ab.hip, profiles/r05b_occupancy_ab.txt, r05i_occupancy_wide.txt,
 //     r05k_occupancy_k8shape.txt, r05l_occupancy_k8lanes.txt): the fastest point is about 64 KiB of
 //     loads in flight per CU, i.e. 4096 / K lanes with one pack each, at ONE workgroup per CU
-//       K = 4 (every type but fp16, mixed there): U = 1, B = 1024 — 4.2 % faster than the two
-//         workgroups per CU its registers allow, and +0.5-4 % over 4 x 256 (profiles/r02_geom_sweep_*);
+//       K = 4-5 (every type but fp16, mixed there at K = 4): U = 1, B = 1024 — at K = 4 4.2 % faster than
+//         the two workgroups per CU its registers allow and +0.5-4 % over 4 x 256
+//         (profiles/r02_geom_sweep_*); at K = 5 3.3-3.4 % over 4 x 256 (fp32, bf16, 1.5 GiB streamed;
+//         profiles/r05zp_occupancy_k35.txt). K = 3 keeps 4 x 256: 1 x 1024 gained 2.9 % at 1 GiB with one
+//         destination but lost 1.2-5.8 % at 96-300 MiB with 2-5 (profiles/r05zr_occupancy_k3m.txt), where
+//         the nt-store table of pickPolicy (nexr_api.cpp) puts those calls under this policy;
 //       K >= 6: U = 1, B = 512 — fp16 K = 8 2.5-2.7 % and fp32 K = 8 3.6 % faster than 1 x 1024, fp32
 //         K = 6 1.3 %; 256 lanes are 10-20 % slower, 384 or 640 lanes 2 % slower;
 //       bf16, K >= 6: U = 1, B = 1024 — its fold is ~15x the VALU of fp16's, and 512 lanes per CU do not
@@ -155,7 +159,7 @@ __host__ __device__ constexpr Shape shape_for(int dt, int k, int pol) {
   return (pol == 3 && k >= 6)                       ? Shape{1, dt == nexrBfloat16 ? 1024 : 512, true}
          : (half && k >= 8)                         ? Shape{1, 1024, false}
          : (k == 4 && pol == 1 && !four)            ? Shape{2, 512, false}
-         : (k == 4 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}
+         : (k >= 4 && k <= 5 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}
                                                     : Shape{4, 256, false};
 }
 __host__ __device__ constexpr int unroll_for(int dt, int k, int pol) { return shape_for(dt, k, pol).u; }

@@ -213,10 +213,16 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
                         (6, 128 << 20, (16384, 256, 4, 3)), (2, 1 << 20, (256, 256, 4, 0))):
         info = nexr.query_launch(k4, [0x60000000], n, dt)
         assert (info.grid, info.block, info.packsPerLane, info.policy) == want, (dt, n)
-    # K = 3 and K = 5 keep the default at every size
+    # K = 3 and K = 5: the default below the nt-store policy; under it K = 5 runs 1 x 1024 at one
+    # workgroup per CU like K = 4 (round 5, fp16 excepted) and K = 3 keeps the default
     for k in (3, 5):
-        info = nexr.query_launch(k4[:3] + [0x50000000] * (k - 3), [0x60000000], 64 << 20, 7)
-        assert (info.block, info.packsPerLane) == (256, 4)
+        srcs_k = k4[:3] + [0x50000000, 0x58000000][:k - 3]
+        info = nexr.query_launch(srcs_k, [0x60000000], 16 << 20, 7)
+        assert (info.block, info.packsPerLane, info.policy) == (256, 4, 1), k
+        info = nexr.query_launch(srcs_k, [0x60000000], 64 << 20, 7)
+        assert (info.block, info.packsPerLane, info.policy) == ((1024, 1, 3) if k == 5 else (256, 4, 3)), k
+        info = nexr.query_launch(srcs_k, [0x60000000], 128 << 20, 6)
+        assert (info.block, info.packsPerLane, info.policy) == (256, 4, 3), k
     # K >= 6 under the nt-store policy (>= 512 MiB streamed): 1 x 512 for every type but bf16, 1 x 1024
     # for bf16 (round 5); below it the default, except 16-bit K = 8, which is 1 x 1024 at every size
     k8 = [0x10000000 * (i + 1) for i in range(8)]

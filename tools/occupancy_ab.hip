@@ -276,6 +276,32 @@ int main(int argc, char** argv) {
                        var<D, OP, K, kPolNtLoad, false, 1, 1024>("nt-ld U1 B1024", 0), var<D, OP, K, kPolNt, false, 1, 1024>("nt-st U1 B1024", 1)}});
     }
   }
+  if (group == "k35") {  // K = 3 and K = 5 under the nt-store policy (default 4 x 256): one workgroup per CU?
+    constexpr int D = nexrFloat32, OP = nexrDevSum, P = kPolNt;
+    cfgs.push_back({"fp32 sum K=3 256 MiB (1 GiB streamed, nt/nt)", 3, 256u << 20, fin,
+                    {var<D, OP, 3, P, false, 4, 256>("U4 B256", 0), var<D, OP, 3, P, false, 1, 1024>("U1 B1024", 1),
+                     var<D, OP, 3, P, false, 2, 512>("U2 B512", 1), var<D, OP, 3, P, false, 1, 512>("U1 B512", 1),
+                     var<D, OP, 3, P, false, 1, 1024>("U1 B1024", 0), var<D, OP, 3, P, false, 4, 256>("U4 B256", 2)}});
+    cfgs.push_back({"fp32 sum K=5 256 MiB (1.5 GiB streamed, nt/nt)", 5, 256u << 20, fin,
+                    {var<D, OP, 5, P, false, 4, 256>("U4 B256", 0), var<D, OP, 5, P, false, 1, 1024>("U1 B1024", 1),
+                     var<D, OP, 5, P, false, 1, 512>("U1 B512", 1), var<D, OP, 5, P, false, 1, 1024>("U1 B1024", 0),
+                     var<D, OP, 5, P, false, 4, 256>("U4 B256", 2)}});
+    constexpr int D2 = nexrBfloat16;
+    cfgs.push_back({"bf16 sum K=5 256 MiB (1.5 GiB streamed, nt/nt)", 5, 256u << 20, fin,
+                    {var<D2, OP, 5, P, false, 4, 256>("U4 B256", 0), var<D2, OP, 5, P, false, 1, 1024>("U1 B1024", 1),
+                     var<D2, OP, 5, P, false, 1, 512>("U1 B512", 1)}});
+  }
+  if (group == "k3m") {  // K = 3 with 2-5 destinations under nt stores (96-512 MiB streamed): 4 x 256 or 1 x 1024 at one per CU
+    constexpr int D = nexrFloat32, OP = nexrDevSum, P = kPolNt;
+    struct KM { int m, mib; };
+    for (KM c : {KM{2, 20}, KM{2, 60}, KM{5, 12}, KM{5, 32}}) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=3 M=%d %d MiB (%d MiB streamed, nt/nt)", c.m, c.mib, (3 + c.m) * c.mib);
+      cfgs.push_back({name, 3, (size_t)c.mib << 20, fin,
+                      {var<D, OP, 3, P, false, 1, 1024>("U1 B1024", 1), var<D, OP, 3, P, false, 4, 256>("U4 B256", 0),
+                       var<D, OP, 3, P, false, 2, 512>("U2 B512", 1)}, c.m});
+    }
+  }
   if (group == "c4sizes") {  // C4's shape by buffer size: is 64 MiB short enough to pay a ramp / tail?
     constexpr int D = nexrInt32, OP = nexrDevMinMax, K = 4;
     for (int mib : {16, 32, 64, 96, 100}) {
