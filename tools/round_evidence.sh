@@ -1,6 +1,8 @@
 #!/bin/bash
 # Reproduce a round's headline evidence on one MI355X in one go (run from the repository root, after
 # build(); every GPU step under its own time limit, chained so the first failure ends the script):
+#   0. a 120 s random parity sweep against the C oracle (tools/fuzz_long.py)
+#                                              -> gpurun_out/evidence_<tag>/fuzz.json
 #   1. the GPU test suite                      -> gpurun_out/evidence_<tag>/gpu_tests.txt
 #   2. smoke()                                 -> .../smoke.txt
 #   3. the default bench line                  -> .../bench.json
@@ -14,6 +16,7 @@ tag=${1:?usage: tools/round_evidence.sh <tag>}
 out=gpurun_out/evidence_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
+timeout -k 10 300 python tools/fuzz_long.py --seconds 120 --max-mib 200 --budget-mib 2000 > "$out/fuzz.json" 2> "$out/fuzz.err" || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > "$out/gpu_tests.txt" 2>&1 || exit 1
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.txt" 2>&1 || exit 1
 timeout -k 10 300 python bench.py > "$out/bench.json" 2> "$out/bench.err" || exit 1
