@@ -35,7 +35,7 @@ extern "C" {
 #define NEXR_API __attribute__((visibility("default")))
 
 #define NEXR_VERSION_MAJOR 0
-#define NEXR_VERSION_MINOR 1
+#define NEXR_VERSION_MINOR 2
 #define NEXR_VERSION_PATCH 0
 
 /* Maximum fan-in / fan-out of one call: srcs[]/dsts[] hold NCCL_MAX_ARITY+1 = 8 entries
@@ -206,13 +206,17 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
  * (src/nccl.h.in:130-133, src/allocator.cc) for the fork's setting, where NEX "device memory" and
  * the transport's staging FIFOs are host memory.
  *   nexrHostRegister    page-locks and device-maps [buff, buff + size) (hipHostRegister, mapped +
- *                       portable) and records it in a process-wide cache sorted by address, like
- *                       the reference's regCache (register.cc:40-60). A range inside one already
- *                       registered here shares that entry (reference count); a range that partly
- *                       overlaps one returns nexrInvalidUsage. *handle identifies the entry.
- *   nexrHostDeregister  drops one reference; the last one unregisters the range (NULL: no-op).
+ *                       portable) and records the pages it touches in a process-wide cache sorted by
+ *                       address, like the reference's regCache (register.cc:40-60). A range inside the
+ *                       pages of an entry already here (registered, or from nexrHostMemAlloc) shares
+ *                       that entry (one more reference); a range that reaches into an entry's pages
+ *                       without lying inside them returns nexrInvalidUsage. *handle is an opaque id
+ *                       that is never reused.
+ *   nexrHostDeregister  drops one reference; the last one unregisters the range (NULL: no-op). A
+ *                       handle with no reference left, or never issued, returns nexrInvalidUsage.
  *   nexrHostMemAlloc    pinned, device-mapped host memory (hipHostMalloc), recorded in the same cache.
- *   nexrHostMemFree     frees memory from nexrHostMemAlloc (NULL: no-op).
+ *   nexrHostMemFree     frees memory from nexrHostMemAlloc (NULL: no-op); nexrInvalidUsage while
+ *                       registrations inside it remain (deregister them first).
  * nexrReduceCopyHost looks every buffer up in this cache first: a buffer wholly inside an entry is
  * read and written in place over PCIe with no runtime query. Other pinned memory (registered by the
  * caller directly) is still found with hipPointerGetAttributes on every call. Do not free or
@@ -334,9 +338,8 @@ NEXR_API nexrResult_t nexrGetSemantics(int* semantics);
  * [0, headElts) and the tail are edge elements (headElts brings dsts[0] to a 128-B boundary when its
  * offset is a whole number of elements) and bodyPacks 16-B packs form the body, pack i being the 16
  * bytes at offset 16 i of every buffer. `unaligned` is 1 when the pointers share no 16-B phase: the
- * body then moves the misaligned buffers with unaligned 16-B accesses. `generic` (the per-element
- * path of round 1) is always 0 and kept for the layout; `unaligned` sits in what was padding, so
- * the struct's size and offsets are unchanged. grid * block never exceeds 2^32 - 1 work items
+ * body then moves the misaligned buffers with unaligned 16-B accesses (ABI 0.2 dropped round 1's
+ * always-zero `generic` field: `unaligned` now sits at offset 16). grid * block never exceeds 2^32 - 1 work items
  * (HIP's launch limit); larger calls grid-stride. policy: 0 plain, 1 non-temporal loads, 3
  * non-temporal loads and stores.
  */
@@ -345,7 +348,6 @@ typedef struct {
   int block;
   int packsPerLane;
   int policy;
-  int generic;
   int unaligned;
   uint64_t headElts;
   uint64_t bodyPacks;

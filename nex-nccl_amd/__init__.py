@@ -110,7 +110,7 @@ class DevRedOpFull(ctypes.Structure):
 class LaunchInfo(ctypes.Structure):
     """Mirror of nexrLaunchInfo (include/nexr.h): what nexrQueryLaunch reports."""
     _fields_ = [("grid", ctypes.c_uint32), ("block", ctypes.c_int), ("packsPerLane", ctypes.c_int),
-                ("policy", ctypes.c_int), ("generic", ctypes.c_int), ("unaligned", ctypes.c_int),
+                ("policy", ctypes.c_int), ("unaligned", ctypes.c_int),
                 ("headElts", ctypes.c_uint64),
                 ("bodyPacks", ctypes.c_uint64)]
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <stdlib.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -217,7 +218,6 @@ void planLayout(RCParams& p, int nSrcs, size_t esz) {
   bool common = (phase16 % esz) == 0;
   for (int s = 1; s < nSrcs && common; s++) common = (((uintptr_t)p.src[s]) & 15) == phase16;
   for (int d = 0; d < p.nDsts && common; d++) common = (((uintptr_t)p.dst[d]) & 15) == phase16;
-  p.generic = 0;
   p.unaligned = common ? 0 : 1;
   uintptr_t phase = (uintptr_t)p.dst[0] & (kLineBytes - 1);
   if (phase % esz) phase = 0;
@@ -895,14 +895,32 @@ uint16_t floatToBf16Rne(float f) {
 // (nexrHostMemAlloc), sorted by begin address. nexrReduceCopyHost looks a buffer up here first, so a
 // call on registered memory costs no HIP query per buffer; because the library made every entry, it
 // also knows when one ends (nexrHostDeregister / nexrHostMemFree), so nothing here goes stale.
+// Entries cover whole pages: hipHostRegister pins and maps every page the range touches, so two
+// buffers that share a page share one entry (the second registration is one more reference), and a
+// range that reaches into an entry's pages without lying inside them is refused (nexrInvalidUsage)
+// instead of failing in the runtime. Handles are monotonic ids, never addresses: a handle whose
+// entry is gone stays invalid even when a later entry lands at the same address.
 struct HostReg {
-  uintptr_t beg = 0, end = 0;
-  char* dev = nullptr;  // device address of beg
-  bool owned = false;   // allocated by nexrHostMemAlloc (freed by nexrHostMemFree), else registered
-  int refs = 1;
+  uintptr_t beg = 0, end = 0;  // the pages: [page floor of the first byte, page end of the last)
+  char* dev = nullptr;         // device address of beg
+  void* hipPtr = nullptr;      // the pointer hipHostRegister / hipHostMalloc returned or took
+  bool owned = false;          // allocated by nexrHostMemAlloc (freed by nexrHostMemFree), else registered
+  int regs = 0;                // live nexrHostRegister references to this entry (its handles)
+  uint64_t id = 0;
 };
 std::shared_mutex gRegMu;
 std::vector<HostReg*> gRegs;  // sorted by beg, non-overlapping
+uint64_t gRegNextId = 1;      // under gRegMu
+
+uintptr_t pageSize() {
+  static const uintptr_t ps = [] {
+    const long v = sysconf(_SC_PAGESIZE);
+    return (uintptr_t)(v > 0 ? v : 4096);
+  }();
+  return ps;
+}
+uintptr_t pageFloor(uintptr_t a) { return a & ~(pageSize() - 1); }
+uintptr_t pageCeil(uintptr_t a) { return (a + pageSize() - 1) & ~(pageSize() - 1); }
 
 // The device address of [p, p + bytes) when the whole range lies inside one entry.
 bool regLookup(const void* p, size_t bytes, void** dev) {
@@ -916,20 +934,28 @@ bool regLookup(const void* p, size_t bytes, void** dev) {
   return true;
 }
 
-// Index of the entry containing [a, a + n), -1 if none; overlap: some entry intersects it.
+// Index of the entry whose pages contain [a, a + n), -1 if none; overlap: some entry's pages
+// intersect the range's pages.
 int regFind(uintptr_t a, size_t n, bool* overlap) {
   *overlap = false;
+  const uintptr_t pb = pageFloor(a), pe = pageCeil(a + n);
   for (size_t i = 0; i < gRegs.size(); i++) {
     const HostReg* r = gRegs[i];
     if (a >= r->beg && a + n <= r->end) return (int)i;
-    if (a < r->end && a + n > r->beg) *overlap = true;
+    if (pb < r->end && pe > r->beg) *overlap = true;
   }
   return -1;
 }
 
 void regInsert(HostReg* r) {
+  r->id = gRegNextId++;
   auto it = std::upper_bound(gRegs.begin(), gRegs.end(), r->beg, [](uintptr_t v, const HostReg* x) { return v < x->beg; });
   gRegs.insert(it, r);
+}
+
+std::vector<HostReg*>::iterator regById(const void* handle) {
+  const uint64_t id = (uint64_t)(uintptr_t)handle;
+  return std::find_if(gRegs.begin(), gRegs.end(), [&](const HostReg* r) { return r->id == id; });
 }
 
 }  // namespace
@@ -986,7 +1012,6 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
   info->block = block;
   info->packsPerLane = unroll_for(datatype, nSrcs, pol);
   info->policy = g.pol;
-  info->generic = 0;
   info->unaligned = p.unaligned;
   info->headElts = p.head;
   info->bodyPacks = p.nPacks;
@@ -1148,15 +1173,16 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
 NEXR_API nexrResult_t nexrHostRegister(void* buff, size_t size, void** handle) {
   if (buff == nullptr || size == 0 || handle == nullptr) return nexrInvalidArgument;
   const uintptr_t a = (uintptr_t)buff;
+  if (a + size < a) return nexrInvalidArgument;
   std::unique_lock<std::shared_mutex> lk(gRegMu);
   bool overlap = false;
   const int i = regFind(a, size, &overlap);
-  if (i >= 0) {  // inside a range this library already registered: share it (register.cc:49-76)
-    gRegs[i]->refs++;
-    *handle = gRegs[i];
+  if (i >= 0) {  // inside pages this library already maps (registered or allocated): share them (register.cc:49-76)
+    gRegs[i]->regs++;
+    *handle = (void*)(uintptr_t)gRegs[i]->id;
     return nexrSuccess;
   }
-  if (overlap) return nexrInvalidUsage;  // partly inside another entry: hipHostRegister would refuse it
+  if (overlap) return nexrInvalidUsage;  // reaches into another entry's pages: hipHostRegister would refuse it
   NEXR_HIP(hipHostRegister(buff, size, hipHostRegisterMapped | hipHostRegisterPortable));
   void* dev = nullptr;
   hipError_t e = hipHostGetDevicePointer(&dev, buff, 0);
@@ -1165,23 +1191,25 @@ NEXR_API nexrResult_t nexrHostRegister(void* buff, size_t size, void** handle) {
     return hipFail(e);
   }
   HostReg* r = new HostReg();
-  r->beg = a;
-  r->end = a + size;
-  r->dev = (char*)dev;
+  r->beg = pageFloor(a);
+  r->end = pageCeil(a + size);
+  r->dev = (char*)dev - (a - r->beg);  // the mapping covers whole pages
+  r->hipPtr = buff;
+  r->regs = 1;
   regInsert(r);
-  *handle = r;
+  *handle = (void*)(uintptr_t)r->id;
   return nexrSuccess;
 }
 
 NEXR_API nexrResult_t nexrHostDeregister(void* handle) {
   if (handle == nullptr) return nexrSuccess;  // ncclCommDeregister accepts a NULL handle
   std::unique_lock<std::shared_mutex> lk(gRegMu);
-  auto it = std::find(gRegs.begin(), gRegs.end(), (HostReg*)handle);
-  if (it == gRegs.end() || (*it)->owned) return nexrInvalidUsage;  // register.cc:150-153
+  auto it = regById(handle);
+  if (it == gRegs.end() || (*it)->regs == 0) return nexrInvalidUsage;  // register.cc:150-153
   HostReg* r = *it;
-  if (--r->refs > 0) return nexrSuccess;
+  if (--r->regs > 0 || r->owned) return nexrSuccess;  // an allocation's pages stay until nexrHostMemFree
   gRegs.erase(it);
-  hipError_t e = hipHostUnregister((void*)r->beg);
+  hipError_t e = hipHostUnregister(r->hipPtr);
   delete r;
   NEXR_HIP(e);
   return nexrSuccess;
@@ -1199,9 +1227,10 @@ NEXR_API nexrResult_t nexrHostMemAlloc(void** ptr, size_t size) {
     return hipFail(e);
   }
   HostReg* r = new HostReg();
-  r->beg = (uintptr_t)host;
-  r->end = (uintptr_t)host + size;
-  r->dev = (char*)dev;
+  r->beg = pageFloor((uintptr_t)host);
+  r->end = pageCeil((uintptr_t)host + size);
+  r->dev = (char*)dev - ((uintptr_t)host - r->beg);
+  r->hipPtr = host;
   r->owned = true;
   std::unique_lock<std::shared_mutex> lk(gRegMu);
   regInsert(r);
@@ -1209,12 +1238,15 @@ NEXR_API nexrResult_t nexrHostMemAlloc(void** ptr, size_t size) {
   return nexrSuccess;
 }
 
+// Refused (nexrInvalidUsage) while registrations inside the allocation remain: their handles would
+// otherwise name freed memory (the caller deregisters first, as ncclCommDeregister before ncclMemFree).
 NEXR_API nexrResult_t nexrHostMemFree(void* ptr) {
   if (ptr == nullptr) return nexrSuccess;
   std::unique_lock<std::shared_mutex> lk(gRegMu);
-  auto it = std::find_if(gRegs.begin(), gRegs.end(), [&](const HostReg* r) { return r->owned && r->beg == (uintptr_t)ptr; });
+  auto it = std::find_if(gRegs.begin(), gRegs.end(), [&](const HostReg* r) { return r->owned && r->hipPtr == ptr; });
   if (it == gRegs.end()) return nexrInvalidArgument;
   HostReg* r = *it;
+  if (r->regs > 0) return nexrInvalidUsage;
   gRegs.erase(it);
   delete r;
   NEXR_HIP(hipHostFree(ptr));

@@ -67,7 +67,7 @@ struct Fold {
     if constexpr (OP == nexrDevSumPostDiv) {
       if (post) acc = T::divide(acc, redArg);  // Apply_PostOp<FuncSumPostDiv> :520-539
     }
-    if constexpr (D == nexrFloat16) {
+    if constexpr (T::kCanon) {  // float16 / bfloat16: NaN -> 0x7fff once, after the fold
       if (canon) acc = T::canon(acc);
     }
     return bc<u32x4>(acc);

@@ -17,8 +17,7 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes per workgroup
 //   [head, head + nPacks*EPP)    the packed body: pack i = 16 contiguous bytes of every buffer
 //   [.., nElts)                  tail edge elements (scalar path)
 // When the pointers share a 16-B phase every body access is 16-B aligned; otherwise (`unaligned`)
-// the others are unaligned 16-B accesses. `generic` (every element on the scalar path) is no longer
-// used and stays 0.
+// the others are unaligned 16-B accesses.
 struct RCParams {
   const char* src[NEXR_MAX_SRCS];
   char* dst[NEXR_MAX_DSTS];
@@ -31,7 +30,6 @@ struct RCParams {
   int nDsts;
   int nPreOp;                   // pre-op applies to srcs[s] for s < nPreOp
   int postOp;
-  int generic;
   int unaligned;  // no common 16-B phase: body packs use unaligned 16-B accesses (diagnostics)
 };
 
@@ -139,9 +137,10 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 //         destination but lost 1.2-5.8 % at 96-300 MiB with 2-5 (profiles/r05zr_occupancy_k3m.txt), where
 //         the nt-store table of pickPolicy (nexr_api.cpp) puts those calls under this policy;
 //       K >= 6: U = 1, B = 512 — fp16 K = 8 2.5-2.7 % and fp32 K = 8 3.6 % faster than 1 x 1024, fp32
-//         K = 6 1.3 %; 256 lanes are 10-20 % slower, 384 or 640 lanes 2 % slower;
-//       bf16, K >= 6: U = 1, B = 1024 — its fold is ~15x the VALU of fp16's, and 512 lanes per CU do not
-//         hide it (2.9 % slower than 1024);
+//         K = 6 1.3 %; 256 lanes are 10-20 % slower, 384 or 640 lanes 2 % slower. bf16 too since round 6:
+//         with the hardware RNE (v_cvt_pk_bf16_f32, nexr_types.hpp) its fold no longer needs 1024 lanes
+//         to hide it, and 1 x 512 is 1.6 % faster than the round-5 fold at 1 x 1024 and level with fp16
+//         and a bare uint32 stream of the same bytes (profiles/r06a_bf16cvt.txt);
 //   - 16-bit floats, K >= 8, below the nt-store policy: U = 1, B = 1024 as the registers admit (two per
 //     CU): rounds 1 and 5 chose 1 x 1024 over 4 x 256 (profiles/r01s3_*_geometry_ab.txt); held to one
 //     workgroup per CU it is 3.2-9.3 % slower under nt loads (64-512 MiB streamed) and equal under plain
@@ -156,7 +155,7 @@ struct Shape {
 __host__ __device__ constexpr Shape shape_for(int dt, int k, int pol) {
   const bool half = dt == nexrFloat16 || dt == nexrBfloat16;
   const bool four = dt == nexrInt32 || dt == nexrUint32 || dt == nexrFloat32;
-  return (pol == 3 && k >= 6)                       ? Shape{1, dt == nexrBfloat16 ? 1024 : 512, true}
+  return (pol == 3 && k >= 6)                       ? Shape{1, 512, true}
          : (half && k >= 8)                         ? Shape{1, 1024, false}
          : (k == 4 && pol == 1 && !four)            ? Shape{2, 512, false}
          : (k >= 4 && k <= 5 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}

@@ -170,14 +170,25 @@ __global__ __launch_bounds__(block_for(D, K, POL)) void reduce_copy_batch_kernel
 }
 
 // A kernel launched with more than 64 KiB of dynamic LDS must be allowed it first, once per device.
-static hipError_t allow_lds(const void* fn, int lds, std::atomic<uint64_t>& allowed) {
+// The attribute applies to the function on the CURRENT device, while the launch runs on the stream's:
+// so it is set on the stream's device (switching to it for the call when the caller's current device
+// differs) and recorded per that device.
+static hipError_t allow_lds(const void* fn, int lds, std::atomic<uint64_t>& allowed, hipStream_t s) {
   if (lds <= 64 * 1024) return hipSuccess;
   int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
+  hipError_t e = hipStreamGetDevice(s, &dev);
   if (e != hipSuccess) return e;
   const uint64_t bit = dev < 64 ? 1ull << dev : 0;
   if (bit && (allowed.load(std::memory_order_acquire) & bit)) return hipSuccess;
+  int cur = 0;
+  e = hipGetDevice(&cur);
+  if (e != hipSuccess) return e;
+  if (cur != dev && (e = hipSetDevice(dev)) != hipSuccess) return e;
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (cur != dev) {
+    const hipError_t back = hipSetDevice(cur);
+    if (e == hipSuccess) e = back;
+  }
   if (e == hipSuccess && bit) allowed.fetch_or(bit, std::memory_order_acq_rel);
   return e;
 }
@@ -198,7 +209,7 @@ static hipError_t launch_k(const RCParams& p, const Geometry& g, hipStream_t s) 
   const int lds = lds_for(D, K, g.pol);
   if (lds > 64 * 1024) {
     static std::atomic<uint64_t> allowed[2][4];  // [isMin][policy]: devices the attribute is set on
-    const hipError_t e = allow_lds(fn, lds, allowed[fn == kernel_for<D, OP, K, false>(g.pol) ? 0 : 1][g.pol & 3]);
+    const hipError_t e = allow_lds(fn, lds, allowed[fn == kernel_for<D, OP, K, false>(g.pol) ? 0 : 1][g.pol & 3], s);
     if (e != hipSuccess) return e;
   }
   void* args[] = {const_cast<RCParams*>(&p)};
@@ -237,7 +248,7 @@ static hipError_t launch_batch_k(const BatchParams& b, int pol, int grid, hipStr
   const int lds = lds_for(D, K, pol);
   if (lds > 64 * 1024) {
     static std::atomic<uint64_t> allowed[2][4];
-    const hipError_t e = allow_lds(fn, lds, allowed[fn == batch_kernel_for<D, OP, K, false>(pol) ? 0 : 1][pol & 3]);
+    const hipError_t e = allow_lds(fn, lds, allowed[fn == batch_kernel_for<D, OP, K, false>(pol) ? 0 : 1][pol & 3], s);
     if (e != hipSuccess) return e;
   }
   void* args[] = {const_cast<BatchParams*>(&b)};

@@ -177,7 +177,7 @@ __device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64
     if constexpr (OP == nexrDevSumPostDiv) {
       if (a.postOp) d[u] = bc<u32x4>(T::divide(bc<V>(d[u]), a.redArg));
     }
-    if constexpr (D == nexrFloat16) {
+    if constexpr (T::kCanon) {
       // ncclFromFloat canonicalises NaN whenever arithmetic ran on the pack
       const bool arith = !a.firstWins && ((a.nRecv >= 1 && a.src) || a.nRecv >= 2 ||
                                           (OP == nexrDevPreMulSum && a.src && a.srcIsInput));
@@ -349,7 +349,7 @@ __device__ __forceinline__ void ll128_tile(const LL128Params& a, uint64_t tile, 
     if constexpr (OP == nexrDevSumPostDiv) {
       if (a.postOp) d[u] = bc<u32x4>(T::divide(bc<V>(d[u]), a.redArg));
     }
-    if constexpr (D == nexrFloat16) {
+    if constexpr (T::kCanon) {
       const bool arith = !a.firstWins && ((a.nRecv >= 1 && a.src) || a.nRecv >= 2 ||
                                           (OP == nexrDevPreMulSum && a.src && a.srcIsInput));
       if (arith) d[u] = bc<u32x4>(T::canon(bc<V>(d[u])));

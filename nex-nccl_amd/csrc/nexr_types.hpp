@@ -16,6 +16,7 @@ typedef int8_t i8x16 __attribute__((ext_vector_type(16)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef int16_t i16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
@@ -37,7 +38,8 @@ __device__ __forceinline__ To bc(From x) {
 //   add/mul  : ncclAdd / ncclMultiply          (reduce_kernel.h:238-248, :317-368)
 //   min/max  : isMin ? (v<c?v:c) : (v>c?v:c)   (reduce_kernel.h:455-478), c = acc, v = new operand
 //   splat    : ncclDecodeScalar<T>(raw)        (reduce_kernel.h:218-236, :317-345) broadcast
-//   canon    : float16 only — ncclFromFloat maps every NaN to 0x7fff (CUDA __float2half host path)
+//   canon    : float16 / bfloat16 (kCanon) — ncclFromFloat maps every NaN to 0x7fff (CUDA
+//              __float2half / __float2bfloat16_rn host path), applied once after the fold
 //   divide   : FuncSumPostDiv::divide          (reduce_kernel.h:83-97), integers only
 // ---------------------------------------------------------------------------------------------
 template <int D> struct Ty;
@@ -50,6 +52,7 @@ struct IntTy {
   using V = UV;
   static constexpr int EPP = N;
   static constexpr bool kIsInt = true;
+  static constexpr bool kCanon = false;
   __device__ static V add(V a, V b) { return a + b; }
   __device__ static V mul(V a, V b) { return a * b; }
   __device__ static V vmin(V c, V v) {
@@ -103,6 +106,7 @@ template <> struct Ty<nexrFloat32> {
   using V = f32x4;
   static constexpr int EPP = 4;
   static constexpr bool kIsInt = false;
+  static constexpr bool kCanon = false;
   __device__ static V add(V a, V b) { return a + b; }
   __device__ static V mul(V a, V b) { return a * b; }
   __device__ static V vmin(V c, V v) { return v < c ? v : c; }
@@ -116,6 +120,7 @@ template <> struct Ty<nexrFloat64> {
   using V = f64x2;
   static constexpr int EPP = 2;
   static constexpr bool kIsInt = false;
+  static constexpr bool kCanon = false;
   __device__ static V add(V a, V b) { return a + b; }
   __device__ static V mul(V a, V b) { return a * b; }
   __device__ static V vmin(V c, V v) { return v < c ? v : c; }
@@ -134,6 +139,7 @@ template <> struct Ty<nexrFloat16> {
   using V = f16x8;
   static constexpr int EPP = 8;
   static constexpr bool kIsInt = false;
+  static constexpr bool kCanon = true;
   __device__ static V add(V a, V b) { return a + b; }
   __device__ static V mul(V a, V b) { return a * b; }
   __device__ static V vmin(V c, V v) { return v < c ? v : c; }
@@ -147,19 +153,20 @@ template <> struct Ty<nexrFloat16> {
 };
 
 // bfloat16: computed in f32 and rounded back to bf16 after every step with round-to-nearest-even,
-// every NaN to 0x7fff (CUDA __float2bfloat16_rn host path, reduce_kernel.h:352-367).
+// every NaN to 0x7fff (CUDA __float2bfloat16_rn host path, reduce_kernel.h:352-367). The rounding is
+// gfx950's v_cvt_pk_bf16_f32 (RNE, two elements per instruction; f32 denormals are kept, so bf16
+// subnormals round as IEEE says). It keeps a NaN's payload where the reference writes 0x7fff: canon()
+// fixes that once after the fold, which gives the same bytes because a NaN accumulator stays NaN
+// through every op (add, mul, and the ternary min/max, which keeps the accumulator when either side is
+// NaN and drops a NaN operand whatever its bits). Round 5's integer RNE with a NaN select after every
+// step cost 4 VALU per element per step.
 template <> struct Ty<nexrBfloat16> {
   using V = u16x8;
   static constexpr int EPP = 8;
   static constexpr bool kIsInt = false;
+  static constexpr bool kCanon = true;
   __device__ static f32x8 widen(V x) { return bc<f32x8>(__builtin_convertvector(x, u32x8) << 16); }
-  __device__ static V narrow(f32x8 f) {
-    u32x8 u = bc<u32x8>(f);
-    u32x8 r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-    i32x8 isnan = (u & 0x7fffffffu) > 0x7f800000u;
-    r = isnan ? (u32x8)0x7fffu : r;
-    return __builtin_convertvector(r, V);
-  }
+  __device__ static V narrow(f32x8 f) { return bc<V>(__builtin_convertvector(f, bf16x8)); }
   __device__ static V add(V a, V b) { return narrow(widen(a) + widen(b)); }
   __device__ static V mul(V a, V b) { return narrow(widen(a) * widen(b)); }
   __device__ static V vmin(V c, V v) {
@@ -171,7 +178,10 @@ template <> struct Ty<nexrBfloat16> {
     return narrow(fv > fc ? fv : fc);
   }
   __device__ static V splat(uint64_t raw) { return (V)((uint16_t)raw); }
-  __device__ static V canon(V x) { return x; }
+  __device__ static V canon(V x) {
+    const i16x8 isnan = (x & (uint16_t)0x7fff) > (uint16_t)0x7f80;
+    return isnan ? (V)(uint16_t)0x7fff : x;
+  }
   __device__ static V divide(V x, uint64_t) { return x; }
 };
 

@@ -59,7 +59,7 @@ def test_type_size_and_strings(nexr):
         assert L.nexrTypeSize(int(dt)) == sz
     assert L.nexrTypeSize(12) == 0
     assert L.nexrGetErrorString(4) == b"invalid argument"
-    assert nexr.version() == 100
+    assert nexr.version() == 200
 
 
 def _call(nexr, nsrcs=2, ndsts=1, n=16, dt=7, op=0, arg=0, pre=None, srcs=None, dsts=None):
@@ -185,7 +185,7 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     take the packed path too (unaligned 16-B accesses), never an element-per-work-item path."""
     # int8, K=2, mixed phases: packed, unaligned; 1 TiB per buffer needs 2^32 workgroups of 256
     info = nexr.query_launch([0x1000, 0x2001], [0x3000], 1 << 40, 0)
-    assert (info.generic, info.unaligned, info.block, info.packsPerLane) == (0, 1, 256, 4)
+    assert (info.unaligned, info.block, info.packsPerLane) == (1, 256, 4)
     assert info.grid * info.block <= 0xFFFFFFFF
     assert info.grid == 0xFFFFFFFF // 256
     info = nexr.query_launch([0x1000, 0x2001], [0x3000], 1 << 32, 0)
@@ -194,11 +194,11 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     # 2^23 cap
     srcs = [0x10000 * (i + 1) for i in range(8)]
     info = nexr.query_launch(srcs, [0x100000], 8 << 30, 6)
-    assert info.generic == 0 and info.block == 512 and info.packsPerLane == 1
+    assert info.block == 512 and info.packsPerLane == 1
     assert info.grid == (8 << 30) * 2 // 16 // 512 and info.grid * info.block <= 0xFFFFFFFF
     # fp16 K=8 with mixed phases at 2^33 elements: packed like the aligned call above
     info = nexr.query_launch([0x10000 * (i + 1) + (i & 1) * 2 for i in range(8)], [0x100000], 1 << 33, 6)
-    assert (info.generic, info.unaligned) == (0, 1) and info.grid == (1 << 34) // 16 // 512
+    assert info.unaligned == 1 and info.grid == (1 << 34) // 16 // 512
     # C2 geometry: 256 MiB fp32 K=2, U=4 packs per lane, one 16 KiB trip per workgroup, nt loads
     info = nexr.query_launch([0x10000000, 0x20000000], [0x30000000], 64 << 20, 7)
     assert (info.grid, info.block, info.packsPerLane, info.policy) == (16384, 256, 4, 3)
@@ -223,12 +223,12 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
         assert (info.block, info.packsPerLane, info.policy) == ((1024, 1, 3) if k == 5 else (256, 4, 3)), k
         info = nexr.query_launch(srcs_k, [0x60000000], 128 << 20, 6)
         assert (info.block, info.packsPerLane, info.policy) == (256, 4, 3), k
-    # K >= 6 under the nt-store policy (>= 512 MiB streamed): 1 x 512 for every type but bf16, 1 x 1024
-    # for bf16 (round 5); below it the default, except 16-bit K = 8, which is 1 x 1024 at every size
+    # K >= 6 under the nt-store policy (>= 512 MiB streamed): 1 x 512 for every type (bf16 too since
+    # round 6's hardware RNE); below it the default, except 16-bit K = 8, which is 1 x 1024 at every size
     k8 = [0x10000000 * (i + 1) for i in range(8)]
     for k, dt, n, want in ((6, 7, 64 << 20, (32768, 512, 1, 3)), (8, 2, 64 << 20, (32768, 512, 1, 3)),
-                           (7, 8, 32 << 20, (32768, 512, 1, 3)), (8, 9, 128 << 20, (16384, 1024, 1, 3)),
-                           (6, 9, 128 << 20, (16384, 1024, 1, 3)), (8, 6, 128 << 20, (32768, 512, 1, 3)),
+                           (7, 8, 32 << 20, (32768, 512, 1, 3)), (8, 9, 128 << 20, (32768, 512, 1, 3)),
+                           (6, 9, 128 << 20, (32768, 512, 1, 3)), (8, 6, 128 << 20, (32768, 512, 1, 3)),
                            (8, 7, 4 << 20, (1024, 256, 4, 1)), (6, 0, 1 << 20, (64, 256, 4, 0)),
                            (8, 9, 1 << 20, (128, 1024, 1, 0)), (8, 6, 8 << 20, (1024, 1024, 1, 1))):
         info = nexr.query_launch(k8[:k], [0x90000000], n, dt)
@@ -250,17 +250,18 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     # head/body/tail split for a shared 4-B phase: the head brings dst0 to its next 128-B boundary
     # (31 fp32 elements), then 17 packs, then 1 tail element
     info = nexr.query_launch([0x1004, 0x2004], [0x3004], 100, 7)
-    assert (info.generic, info.unaligned, info.headElts, info.bodyPacks) == (0, 0, 31, 17)
+    assert (info.unaligned, info.headElts, info.bodyPacks) == (0, 31, 17)
     # mixed phases, dst0 already on a 128-B boundary: no head, 6 unaligned packs, 4 tail bytes
     info = nexr.query_launch([0x1000, 0x2001], [0x3080], 100, 0)
     assert (info.unaligned, info.headElts, info.bodyPacks) == (1, 0, 6)
     # dst0 not on an element boundary (fp32 at an odd address): no head, all 16-B accesses unaligned
     info = nexr.query_launch([0x1000, 0x2000], [0x3001], 100, 7)
     assert (info.unaligned, info.headElts, info.bodyPacks) == (1, 0, 25)
-    # the diagnostics struct keeps round 1's size and offsets (`unaligned` took the padding)
+    # the diagnostics struct of ABI 0.2 (round 1's always-zero `generic` field dropped)
     import ctypes
     L = nexr.LaunchInfo
-    assert ctypes.sizeof(L) == 40 and L.generic.offset == 16 and L.unaligned.offset == 20
+    assert ctypes.sizeof(L) == 40 and L.policy.offset == 12 and L.unaligned.offset == 16
+    assert not hasattr(L, "generic")
     assert L.headElts.offset == 24 and L.bodyPacks.offset == 32
     # validation as nexrReduceCopy; empty calls launch nothing
     with pytest.raises(nexr.NexrError):

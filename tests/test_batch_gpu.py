@@ -90,8 +90,10 @@ def test_batch_mixed_works_match_oracle(nexr, oracle, dt, dev):
             w.check((mg.DT_NAMES[dt], name, i, w.n))
 
 
-def test_batch_min_and_max_in_one_launch(nexr, oracle, dev):
-    # MinMax carries min/max in each work's redOpArg (reduce_kernel.h:64), so one launch mixes them.
+def test_batch_min_and_max_in_one_call(nexr, oracle, dev):
+    # MinMax carries min/max in each work's redOpArg (reduce_kernel.h:64). The kernel is compiled per
+    # isMin, so reduceCopyBatch runs a mixed batch as two launches, the min works and the
+    # max works (nexr_api.cpp reduceCopyBatch); every work must still get its own op's result.
     rng = np.random.default_rng(7)
     for dt in (mg.I8, mg.U32, mg.F16, mg.F64):
         works = []

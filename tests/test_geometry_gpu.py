@@ -91,9 +91,9 @@ def test_k4_policy_geometries_edges(nexr, oracle, dev, dt, op, name, buf_mib):
                                  [0x900000 + (offs[4] if offs else 0)], n, dt)
         if offs is None or len(set(offs)) == 1:
             if info.policy == 1:
-                assert info.generic == 0 and info.block == (256 if esz == 4 else 512)
+                assert info.block == (256 if esz == 4 else 512)
             else:
-                assert info.generic == 0 and info.block == (256 if dt == mg.F16 else 1024)
+                assert info.block == (256 if dt == mg.F16 else 1024)
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
         got = _run(nexr, srcs, dt, op, arg, offs)
         assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)
@@ -172,12 +172,12 @@ def test_wide_fan_in_nt_store_geometry_edges(nexr, oracle, dev, dt, k, op, name,
 
 @pytest.mark.parametrize("dt,k", [(mg.F16, 8), (mg.BF16, 6)])
 def test_16bit_wide_fan_in_nt_store_geometry(nexr, oracle, dev, dt, k):
-    """fp16 K = 8 at >= 512 MiB streamed runs 512 lanes, bf16 K >= 6 1024 lanes (its fold's VALU), both one
-    pack per lane at one workgroup per CU; a size just past a trip boundary, against the oracle."""
+    """fp16 K = 8 and bf16 K >= 6 at >= 512 MiB streamed run 512 lanes (bf16 since round 6's hardware
+    RNE), one pack per lane at one workgroup per CU; a size just past a trip boundary, against the oracle."""
     n = 40 * MIB + 8 * 512 * 2 + 3  # 80 MiB per buffer: >= 512 MiB streamed for K >= 6
     srcs = mg.gen_inputs(dt, k, n, 6100 + k, special=True)
     info = nexr.query_launch([0x1000000 * (i + 1) for i in range(k)], [0x9000000], n, dt)
-    assert (info.policy, info.block, info.packsPerLane) == (3, 512 if dt == mg.F16 else 1024, 1)
+    assert (info.policy, info.block, info.packsPerLane) == (3, 512, 1)
     exp = oracle.reduce_copy(srcs, 1, dt, mg.SUM, 0, threads=16)[0]
     assert mg.canon_bytes(dt, _run(nexr, srcs, dt, mg.SUM, 0)) == mg.canon_bytes(dt, exp)
 
@@ -245,3 +245,27 @@ def test_k5_nt_store_geometry_edges(nexr, oracle, dev, dt, k, op, name, buf_mib)
         assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)
         del srcs, exp, got
         torch.cuda.empty_cache()
+
+
+def test_lds_reserving_launch_on_another_devices_stream(nexr, oracle):
+    """Advisor r5 (low): the one-workgroup-per-CU shapes launch with 120 KiB of dynamic LDS, which the
+    kernel must be allowed first; HIP applies that attribute on the CURRENT device, so the library sets
+    it on the stream's device. First launch of a fresh (datatype, K, policy) on a device-1 stream while
+    device 0 is current: exact (needs two GPUs)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    n = (600 << 20) // 9 // 2 // 16 * 16  # fp16 K = 8, > 512 MiB streamed: nt stores, 1 x 512 at one per CU
+    srcs = mg.gen_inputs(mg.F16, 8, 4099, 9100, special=True)
+    exp = oracle.reduce_copy(srcs, 1, mg.F16, mg.SUM, 0)[0]
+    torch.cuda.set_device(0)
+    d1 = torch.device("cuda:1")
+    reps = n // 4099 + 1
+    bufs = [torch.from_numpy(np.tile(s, reps)[:n].view(np.uint8).copy()).to(d1) for s in srcs]
+    out = torch.full((n * 2,), 0x5A, dtype=torch.uint8, device=d1)
+    s1 = torch.cuda.Stream(device=d1)
+    nexr.reduce_copy_ptrs([b.data_ptr() for b in bufs], [out.data_ptr()], n, mg.F16, mg.SUM, 0, None, False,
+                          s1.cuda_stream)
+    s1.synchronize()
+    assert torch.cuda.current_device() == 0
+    got = out[:4099 * 2].cpu().numpy().view(np.float16)
+    assert mg.canon_bytes(mg.F16, got) == mg.canon_bytes(mg.F16, exp)

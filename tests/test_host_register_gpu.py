@@ -221,3 +221,97 @@ def test_buffer_past_a_registered_range_is_staged(hip):
         assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
     finally:
         nexr.host_deregister(h)
+
+
+def test_register_inside_an_allocation_then_free(hip):
+    """Advisor r5 (medium): memory from nexrHostMemAlloc may be registered (the reference's
+    ncclMemAlloc-then-ncclCommRegister pattern). The registration is one more reference on the
+    allocation's entry that nexrHostDeregister drops; nexrHostMemFree refuses while it is live; a
+    handle whose entry is gone stays invalid, even after a new allocation lands at the same address
+    (handles are ids, not addresses)."""
+    nexr = importlib.import_module("nex-nccl_amd")
+    n = 4099
+    p = nexr.host_mem_alloc(3 * 4 * n + 64)
+    h = nexr.host_register(p + 16, 2 * 4 * n)
+    h2 = nexr.host_register(p + 32, 64)  # the same entry: one more reference
+    assert h == h2 and h not in (0, p)
+    with pytest.raises(nexr.NexrError) as e:
+        nexr.host_mem_free(p)  # registrations inside it remain
+    assert e.value.code == 5
+    a = np.ctypeslib.as_array((ctypes.c_float * n).from_address(p + 16))
+    b = np.ctypeslib.as_array((ctypes.c_float * n).from_address(p + 16 + 4 * n))
+    out = np.ctypeslib.as_array((ctypes.c_float * n).from_address(p + 16 + 8 * n))
+    rng = np.random.default_rng(21)
+    _fill(rng, a)
+    _fill(rng, b)
+    out[:] = np.nan
+    nexr.host_path_stats(reset=True)
+    nexr.reduce_copy_ptrs([p + 16, p + 16 + 4 * n], [p + 16 + 8 * n], n, 7, 0, host=True)
+    st = nexr.host_path_stats()
+    assert (st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (1, 3, 0), st
+    assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+    nexr.host_deregister(h)
+    nexr.host_deregister(h2)
+    with pytest.raises(nexr.NexrError) as e:
+        nexr.host_deregister(h)  # no reference left
+    assert e.value.code == 5
+    nexr.host_mem_free(p)
+    q = nexr.host_mem_alloc(3 * 4 * n + 64)  # possibly at p again
+    try:
+        with pytest.raises(nexr.NexrError) as e:
+            nexr.host_deregister(h)  # the old handle names nothing, whatever q's address
+        assert e.value.code == 5
+        hq = nexr.host_register(q, 64)
+        assert hq != h
+        nexr.host_deregister(hq)
+    finally:
+        nexr.host_mem_free(q)
+    with pytest.raises(nexr.NexrError) as e:
+        nexr.host_deregister(12345678)  # never issued
+    assert e.value.code == 5
+
+
+def test_sub_page_neighbours_share_one_entry(hip):
+    """Advisor r5 (low): hipHostRegister pins whole pages, so two disjoint buffers in one page cannot be
+    registered twice with the runtime. The second registration shares the first one's entry (one
+    handle, two references), a call on the second buffer is read in place from the cache, and only the
+    last deregistration unpins the page. A range reaching into the entry's pages from outside is
+    refused with nexrInvalidUsage, not a raw HIP error."""
+    nexr = importlib.import_module("nex-nccl_amd")
+    reg = Region(hip, 4 * 4096, register=False)
+    n = 100
+    try:
+        ha = nexr.host_register(reg.base + 4096 + 16, 4 * n)       # buffer A in page 1
+        hb = nexr.host_register(reg.base + 4096 + 2048, 8 * n)     # buffer B, same page, disjoint
+        assert ha == hb
+        with pytest.raises(nexr.NexrError) as e:  # from page 0 into page 1
+            nexr.host_register(reg.base + 4000, 200)
+        assert e.value.code == 5
+        a = reg.f32(4096 + 2048, n)
+        b = reg.f32(4096 + 2048 + 4 * n, n)
+        out = reg.f32(4096 + 16, n)  # A's bytes: same page, read in place too
+        rng = np.random.default_rng(22)
+        _fill(rng, a)
+        _fill(rng, b)
+        out[:] = np.nan
+        nexr.host_path_stats(reset=True)
+        nexr.reduce_copy_ptrs([reg.base + 4096 + 2048, reg.base + 4096 + 2048 + 4 * n], [reg.base + 4096 + 16], n, 7, 0,
+                              host=True)
+        st = nexr.host_path_stats()
+        assert (st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (1, 3, 0), st
+        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+        nexr.host_deregister(ha)
+        nexr.host_path_stats(reset=True)
+        nexr.reduce_copy_ptrs([reg.base + 4096 + 2048, reg.base + 4096 + 2048 + 4 * n], [reg.base + 4096 + 16], n, 7, 0,
+                              host=True)
+        assert nexr.host_path_stats()["registeredHits"] == 3  # B's reference keeps the page
+        nexr.host_deregister(hb)
+        nexr.host_path_stats(reset=True)
+        out[:] = np.nan
+        nexr.reduce_copy_ptrs([reg.base + 4096 + 2048, reg.base + 4096 + 2048 + 4 * n], [reg.base + 4096 + 16], n, 7, 0,
+                              host=True)
+        st = nexr.host_path_stats()
+        assert (st["zeroCopyCalls"], st["registeredHits"]) == (0, 0), st
+        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+    finally:
+        reg.close()

@@ -26,5 +26,5 @@ for name, (oa, ob, oo) in {"aligned": (0, 0, 0), "shared phase 4B": (4, 4, 4), "
     for i in range(20): launch(i)
     e1.record(s); e1.synchronize()
     us = e0.elapsed_time(e1) / 20 * 1e3
-    print(f"{name:<18} generic={info.generic} grid={info.grid} block={info.block} {us:8.1f} us {3*nn*esz/us/1e3:8.1f} GB/s", flush=True)
+    print(f"{name:<18} grid={info.grid} block={info.block} {us:8.1f} us {3*nn*esz/us/1e3:8.1f} GB/s", flush=True)
     del sets; torch.cuda.empty_cache()

@@ -31,6 +31,39 @@
 
 using namespace nexr;
 
+// Round 5's bfloat16 fold, kept verbatim here as the A/B baseline of the round-6 one (group "bf16cvt"):
+// integer RNE with a NaN select after every step (nexr_types.hpp at 3c2cdf3).
+constexpr int kBf16IntRne = 100;
+namespace nexr {
+template <> struct Ty<kBf16IntRne> {
+  using V = u16x8;
+  static constexpr int EPP = 8;
+  static constexpr bool kIsInt = false;
+  static constexpr bool kCanon = false;
+  __device__ static f32x8 widen(V x) { return bc<f32x8>(__builtin_convertvector(x, u32x8) << 16); }
+  __device__ static V narrow(f32x8 f) {
+    u32x8 u = bc<u32x8>(f);
+    u32x8 r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+    i32x8 isnan = (u & 0x7fffffffu) > 0x7f800000u;
+    r = isnan ? (u32x8)0x7fffu : r;
+    return __builtin_convertvector(r, V);
+  }
+  __device__ static V add(V a, V b) { return narrow(widen(a) + widen(b)); }
+  __device__ static V mul(V a, V b) { return narrow(widen(a) * widen(b)); }
+  __device__ static V vmin(V c, V v) {
+    f32x8 fc = widen(c), fv = widen(v);
+    return narrow(fv < fc ? fv : fc);
+  }
+  __device__ static V vmax(V c, V v) {
+    f32x8 fc = widen(c), fv = widen(v);
+    return narrow(fv > fc ? fv : fc);
+  }
+  __device__ static V splat(uint64_t raw) { return (V)((uint16_t)raw); }
+  __device__ static V canon(V x) { return x; }
+  __device__ static V divide(V x, uint64_t) { return x; }
+};
+}  // namespace nexr
+
 __global__ void fill_bits(uint32_t* p, size_t n, uint64_t seed, uint32_t mask) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
@@ -369,6 +402,46 @@ int main(int argc, char** argv) {
                       {var<D, OP, K, P, false, 2, 512>("U2 B512", 0, 0x7f), var<D, OP, K, P, false, 1, 512>("U1 B512", 1, 0x7f),
                        var<D, OP, K, P, false, 1, 512>("U1 B512", 2, 0x7f), var<D, OP, K, P, false, 2, 512>("U2 B512", 2, 0x7f)}});
     }
+  }
+  if (group == "bf16cvt") {  // round 6: bf16 through v_cvt_pk_bf16_f32 + one final NaN canonicalisation
+    constexpr int D = nexrBfloat16, D0 = kBf16IntRne, OP = nexrDevSum, K = 8, P = kPolNt;
+    cfgs.push_back({"C3 bf16 sum K=8 256 MiB (nt/nt): hardware cvt (hw) vs round-5 integer RNE (int), lanes per CU", K,
+                    256u << 20, fin,
+                    {var<D0, OP, K, P, false, 1, 1024>("int U1 B1024", 1), var<D, OP, K, P, false, 1, 1024>("hw U1 B1024", 1),
+                     var<D, OP, K, P, false, 1, 512>("hw U1 B512", 1), var<D, OP, K, P, false, 1, 512>("hw U1 B512", 2),
+                     var<D0, OP, K, P, false, 1, 512>("int U1 B512", 2), var<D, OP, K, P, false, 2, 512>("hw U2 B512", 1),
+                     var<D, OP, K, P, false, 1, 256>("hw U1 B256", 4)}});
+    constexpr int F = nexrFloat16;
+    cfgs.push_back({"C3 fp16 sum K=8 256 MiB (nt/nt): production and 2 x 512 per CU", K, 256u << 20, fin,
+                    {var<F, OP, K, P, false, 1, 512>("U1 B512", 1), var<F, OP, K, P, false, 1, 512>("U1 B512", 2),
+                     var<F, OP, K, P, false, 1, 256>("U1 B256", 4)}});
+    constexpr int W = nexrUint32;
+    cfgs.push_back({"uint32 sum K=8 256 MiB (nt/nt): the same bytes, bare stream", K, 256u << 20, all,
+                    {var<W, OP, K, P, false, 1, 512>("U1 B512", 1), var<W, OP, K, P, false, 1, 512>("U1 B512", 2),
+                     var<W, OP, K, P, false, 1, 1024>("U1 B1024", 1)}});
+    constexpr int D4 = nexrFloat32, K4 = 4;
+    cfgs.push_back({"fp32 sum K=4 256 MiB (nt/nt): 1 x 1024 (production) vs 2 x 512 per CU", K4, 256u << 20, fin,
+                    {var<D4, OP, K4, P, false, 1, 1024>("U1 B1024", 1), var<D4, OP, K4, P, false, 1, 512>("U1 B512", 2),
+                     var<D4, OP, K4, P, false, 2, 512>("U2 B512", 1)}});
+    cfgs.push_back({"bf16 sum K=4 256 MiB (nt/nt): 1 x 1024 (production) vs 2 x 512 per CU", K4, 256u << 20, fin,
+                    {var<D, OP, K4, P, false, 1, 1024>("hw U1 B1024", 1), var<D, OP, K4, P, false, 1, 512>("hw U1 B512", 2),
+                     var<D0, OP, K4, P, false, 1, 1024>("int U1 B1024", 1)}});
+  }
+  if (group == "k45") {  // round 6: K = 4-5 under nt stores, 1 x 1024 at one per CU (production) vs 1 x 512 at two
+    constexpr int P = kPolNt;
+#define K45(D, OP, K, ISMIN, ARG, NAME, MASK)                                                                \
+  cfgs.push_back({NAME " K=" #K " 256 MiB (nt/nt)", K, 256u << 20, MASK,                                     \
+                  {var<D, OP, K, P, ISMIN, 1, 1024>("U1 B1024", 1, ARG), var<D, OP, K, P, ISMIN, 1, 512>("U1 B512", 2, ARG), \
+                   var<D, OP, K, P, ISMIN, 1, 1024>("U1 B1024", 1, ARG)}});
+    K45(nexrFloat32, nexrDevSum, 4, false, 0, "fp32 sum", fin)
+    K45(nexrBfloat16, nexrDevSum, 4, false, 0, "bf16 sum", fin)
+    K45(nexrInt8, nexrDevMinMax, 4, false, 0x7f, "int8 max", all)
+    K45(nexrInt32, nexrDevMinMax, 4, true, 0x80000000ull, "int32 min", all)
+    K45(nexrFloat64, nexrDevSum, 4, false, 0, "fp64 sum", fin)
+    K45(nexrFloat32, nexrDevSum, 5, false, 0, "fp32 sum", fin)
+    K45(nexrBfloat16, nexrDevSum, 5, false, 0, "bf16 sum", fin)
+    K45(nexrUint8, nexrDevProd, 5, false, 0, "uint8 prod", all)
+#undef K45
   }
   if (group == "bench") {
   {
