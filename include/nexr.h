@@ -334,7 +334,8 @@ NEXR_API nexrResult_t nexrGetSemantics(int* semantics);
 
 /*
  * nexrQueryLaunch — diagnostics: the launch nexrReduceCopy would make for these pointers and this
- * size (no GPU work, no device needed; the same validation as nexrReduceCopy with devRedOp = Sum).
+ * size (no GPU work, no device needed; the same validation as nexrReduceCopy with devRedOp = Sum). A
+ * one-source call runs as a byte copy (the uint8 kernel), so its headElts and bodyPacks count bytes.
  * [0, headElts) and the tail are edge elements (headElts brings dsts[0] to a 128-B boundary when its
  * offset is a whole number of elements) and bodyPacks 16-B packs form the body, pack i being the 16
  * bytes at offset 16 i of every buffer. `unaligned` is 1 when the pointers share no 16-B phase: the

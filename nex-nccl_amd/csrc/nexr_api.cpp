@@ -106,6 +106,25 @@ void applySemantics(CallShape& c) {
   }
 }
 
+// The kernel a (semantics-shaped) call runs: kernel_compiled (nexr_internal.h) names the compiled
+// ones; every other call maps onto one of them with the same output bytes. A K = 1 copy becomes a
+// byte copy (*nElts counted in bytes from then on); signed Sum / Prod / PreMulSum / SumPostDiv run the
+// unsigned kernel; PreMulSum without pre-op sources and SumPostDiv without the divide run Sum.
+int unsignedOf(int dt) {
+  return dt == nexrInt8 ? nexrUint8 : dt == nexrInt32 ? nexrUint32 : dt == nexrInt64 ? nexrUint64 : dt;
+}
+void routeKernel(CallShape& c, size_t* nElts) {
+  if (c.op == nexrDevPreMulSum && c.nPreOp == 0) c.op = nexrDevSum;
+  if (c.op == nexrDevSumPostDiv && !c.postOp) c.op = nexrDevSum;
+  if (c.nSrcs == 1 && c.op != nexrDevPreMulSum && c.op != nexrDevSumPostDiv) {
+    *nElts *= typeSize(c.dt);
+    c.dt = nexrUint8;
+    c.op = nexrDevSum;
+    return;
+  }
+  if (c.op != nexrDevMinMax) c.dt = unsignedOf(c.dt);
+}
+
 // The same for an LL / LL128 step (after validation): shipped → every reduce returns its first operand,
 // the peer (prims_ll.h:288-294, prims_ll128.h:225-255), with no pre-op and no post-op.
 void llSemantics(int* dt, int* op, int* srcIsInput, int* postOp, int* firstWins) {
@@ -267,9 +286,14 @@ hipError_t launchBatchDt(int dt, const BatchParams& b, int op, int nSrcs, int po
   return hipErrorInvalidValue;
 }
 
-// One batch launch per (nSrcs, run of <= kMaxBatch works): work i gets
-// max(1, workgroupsFor(work i)) workgroups (its one-shot grid), total capped at gridCap(block) by
-// shrinking the largest shares (the kernel grid-strides inside each work's range).
+nexrResult_t launchSingle(const RCParams& p, int dt, int op, int nSrcs, hipStream_t stream, uint64_t maxGrid);
+
+// One batch launch per run of <= kMaxBatch works that run the same kernel: the works as the semantics
+// and the kernel routing (routeKernel) run them, grouped by (datatype, op, K, and for MinMax isMin),
+// each group in order of first appearance. Work i gets max(1, workgroupsFor(work i)) workgroups (its
+// one-shot grid), total capped at gridCap(block) by shrinking the largest shares (the kernel
+// grid-strides inside each work's range). A run that would stream enough for non-temporal stores runs
+// its works as single launches instead (kBatchPolicies, nexr_internal.h).
 nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int datatype, int op, hipStream_t stream) {
   if (nWorks < 0 || (nWorks > 0 && works == nullptr)) return nexrInvalidArgument;
   for (int i = 0; i < nWorks; i++) {
@@ -278,43 +302,50 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
                               w.preOpArgs);
     if (r != nexrSuccess) return r;
   }
-  std::vector<nexrReduceCopyWork> shaped;  // the works as the semantics run them (applySemantics)
-  if (semantics() != nexrSemanticsNccl && nWorks > 0) {
-    CallShape c0{datatype, op, 1, 0, 0, nullptr};
-    applySemantics(c0);
-    shaped.assign(works, works + nWorks);
-    for (auto& w : shaped) {
-      CallShape c{datatype, op, w.nSrcs, w.nPreOpSrcs, w.postOp, nullptr};
-      applySemantics(c);
-      w.nSrcs = c.nSrcs;
-      w.nPreOpSrcs = c.nPreOp;
-      w.postOp = c.postOp;
-    }
-    works = shaped.data();
-    datatype = c0.dt;
-    op = c0.op;
+  struct Routed {
+    CallShape c;
+    int minClass;  // MinMax: 1 = min ((redOpArg & 1) == 0), 0 = max
+    size_t nElts;
+    const nexrReduceCopyWork* w;
+  };
+  std::vector<Routed> rw;
+  rw.reserve((size_t)nWorks);
+  for (int i = 0; i < nWorks; i++) {
+    const nexrReduceCopyWork& w = works[i];
+    if (w.nElts == 0 || w.nDsts == 0) continue;
+    Routed x{{datatype, op, w.nSrcs, w.nPreOpSrcs, w.postOp, nullptr}, 0, w.nElts, &w};
+    applySemantics(x.c);
+    routeKernel(x.c, &x.nElts);
+    x.minClass = x.c.op == nexrDevMinMax && (w.redOpArg & 1) == 0 ? 1 : 0;
+    rw.push_back(x);
   }
-  const size_t esz = typeSize(datatype);
-  // One run per (K, and for MinMax isMin = (redOpArg & 1) == 0): the kernel is compiled per isMin.
-  const int nMin = op == nexrDevMinMax ? 2 : 1;
-  for (int kk = 0; kk < NEXR_MAX_SRCS * nMin; kk++) {
-    const int k = 1 + kk / nMin;
-    const int minClass = kk % nMin;  // MinMax: 0 = max (arg bit 0 set), 1 = min
+  std::vector<char> taken(rw.size(), 0);
+  for (size_t i0 = 0; i0 < rw.size(); i0++) {
+    if (taken[i0]) continue;
+    const CallShape key = rw[i0].c;
+    const int keyMin = rw[i0].minClass, k = key.nSrcs;
+    const size_t esz = typeSize(key.dt);
     BatchParams b;
     b.nWorks = 0;
     uint64_t blocks[kMaxBatch];
     uint64_t streamBytes = 0;
-    // One launch per run of works: the policy (and with it the geometry) from the bytes the whole
-    // launch streams, then work i gets its one-shot grid, the total capped at gridCap(block) by
-    // halving the largest shares (rare: > 4 G packed items; the kernel grid-strides inside a work).
     auto flush = [&]() -> nexrResult_t {
       if (b.nWorks == 0) return nexrSuccess;
       const int pol = pickPolicy(streamBytes);
-      const int block = block_for(datatype, k, pol);
+      if (pol >= kBatchPolicies) {  // non-temporal stores: one launch per work, each at its own policy
+        for (int i = 0; i < b.nWorks; i++) {
+          nexrResult_t r = launchSingle(b.w[i], key.dt, key.op, k, stream, 0);
+          if (r != nexrSuccess) return r;
+        }
+        b.nWorks = 0;
+        streamBytes = 0;
+        return nexrSuccess;
+      }
+      const int block = block_for(key.dt, k, pol);
       const uint64_t cap = gridCap(block);
       uint64_t total = 0;
       for (int i = 0; i < b.nWorks; i++) {
-        const uint64_t need = workgroupsFor(b.w[i], k, datatype, pol);
+        const uint64_t need = workgroupsFor(b.w[i], k, key.dt, pol);
         blocks[i] = need < 1 ? 1 : (need < cap ? need : cap);
         total += blocks[i];
       }
@@ -331,19 +362,19 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
       Geometry g;
       nexrResult_t r = pickGeometry(total, pol, block, &g);
       if (r != nexrSuccess) return r;
-      NEXR_HIP(launchBatchDt(datatype, b, op, k, g.pol, (int)total, stream));
+      NEXR_HIP(launchBatchDt(key.dt, b, key.op, k, g.pol, (int)total, stream));
       b.nWorks = 0;
       streamBytes = 0;
       return nexrSuccess;
     };
-    for (int i = 0; i < nWorks; i++) {
-      const nexrReduceCopyWork& w = works[i];
-      if (w.nSrcs != k || w.nElts == 0 || w.nDsts == 0) continue;
-      if (nMin == 2 && (int)((w.redOpArg & 1) == 0) != minClass) continue;
-      RCParams& p = b.w[b.nWorks];
-      fillParams(p, k, w.srcs, w.nDsts, w.dsts, w.nElts, esz, w.redOpArg, w.nPreOpSrcs, w.preOpArgs, nullptr,
-                 w.postOp);
-      streamBytes += (uint64_t)(k + w.nDsts) * w.nElts * esz;
+    for (size_t i = i0; i < rw.size(); i++) {
+      const Routed& x = rw[i];
+      if (taken[i] || x.c.dt != key.dt || x.c.op != key.op || x.c.nSrcs != k || x.minClass != keyMin) continue;
+      taken[i] = 1;
+      const nexrReduceCopyWork& w = *x.w;
+      fillParams(b.w[b.nWorks], k, w.srcs, w.nDsts, w.dsts, x.nElts, esz, w.redOpArg, x.c.nPreOp, w.preOpArgs, nullptr,
+                 x.c.postOp);
+      streamBytes += (uint64_t)(k + w.nDsts) * x.nElts * esz;
       if (++b.nWorks == kMaxBatch) {
         nexrResult_t r = flush();
         if (r != nexrSuccess) return r;
@@ -352,6 +383,20 @@ nexrResult_t reduceCopyBatch(const nexrReduceCopyWork* works, int nWorks, int da
     nexrResult_t r = flush();
     if (r != nexrSuccess) return r;
   }
+  return nexrSuccess;
+}
+
+// One launch of a routed call whose parameters are filled: policy by the bytes it streams, one-shot grid
+// (capped at maxGrid when > 0).
+nexrResult_t launchSingle(const RCParams& p, int dt, int op, int nSrcs, hipStream_t stream, uint64_t maxGrid) {
+  const uint64_t esz = (uint64_t)typeSize(dt);
+  const int pol = pickPolicy((uint64_t)(nSrcs + p.nDsts) * p.nElts * esz, nSrcs, p.nDsts);
+  uint64_t wgs = workgroupsFor(p, nSrcs, dt, pol);
+  if (maxGrid > 0 && wgs > maxGrid) wgs = maxGrid;
+  Geometry g;
+  nexrResult_t r = pickGeometry(wgs, pol, block_for(dt, nSrcs, pol), &g);
+  if (r != nexrSuccess) return r;
+  NEXR_HIP(launchDt(dt, p, op, nSrcs, g, stream));
   return nexrSuccess;
 }
 
@@ -375,17 +420,12 @@ nexrResult_t reduceCopyDevice(int nSrcs, const void* const* srcs, int nDsts, voi
   if (nElts == 0 || nDsts == 0) return nexrSuccess;  // common_kernel.h:288-289: nothing to store
   CallShape c{datatype, op, nSrcs, nPreOpSrcs, postOp, prePtr};
   applySemantics(c);
+  size_t n = nElts;
+  routeKernel(c, &n);
   const size_t esz = typeSize(c.dt);
   RCParams p;
-  fillParams(p, c.nSrcs, srcs, nDsts, dsts, nElts, esz, redOpArg, c.nPreOp, preOpArgs, c.prePtr, c.postOp);
-  Geometry g;
-  const int pol = pickPolicy((uint64_t)(c.nSrcs + nDsts) * nElts * esz, c.nSrcs, nDsts);
-  uint64_t wgs = workgroupsFor(p, c.nSrcs, c.dt, pol);
-  if (maxGrid > 0 && wgs > maxGrid) wgs = maxGrid;
-  r = pickGeometry(wgs, pol, block_for(c.dt, c.nSrcs, pol), &g);
-  if (r != nexrSuccess) return r;
-  NEXR_HIP(launchDt(c.dt, p, c.op, c.nSrcs, g, stream));
-  return nexrSuccess;
+  fillParams(p, c.nSrcs, srcs, nDsts, dsts, n, esz, redOpArg, c.nPreOp, preOpArgs, c.prePtr, c.postOp);
+  return launchSingle(p, c.dt, c.op, c.nSrcs, stream, maxGrid);
 }
 
 // ---- independent chunks on several GPUs from one host call -------------------
@@ -999,7 +1039,9 @@ NEXR_API nexrResult_t nexrQueryLaunch(int nSrcs, const void* const* srcs, int nD
   if (nElts == 0 || nDsts == 0) return nexrSuccess;  // nothing would be launched
   CallShape c{datatype, nexrDevSum, nSrcs, 0, 0, nullptr};
   applySemantics(c);
+  routeKernel(c, &nElts);  // a K = 1 call is a byte copy: headElts / bodyPacks of the uint8 kernel
   nSrcs = c.nSrcs;
+  datatype = c.dt;
   const size_t esz = typeSize(datatype);
   RCParams p;
   fillParams(p, nSrcs, srcs, nDsts, dsts, nElts, esz, 0, 0, nullptr, nullptr, 0);

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <deque>
 #include <functional>
 #include <thread>
 #include <vector>
@@ -165,6 +166,7 @@ struct nexrRingComm {
   // then land in a peer GPU's memory, and only the synchronisation is documented to cover them).
   // NEXR_STEP_WAIT=word / sync forces either (stepWaitMode).
   bool stepWaitWord = true;
+  bool lastLLAsync = false;  // whether the last thread-rank ring collective queued its LL steps (diagnostics)
   // Frees what the extras library attached to this communicator (set by its first resident call).
   void (*freeExtras)(nexrRingComm*) = nullptr;
   // Resident ring (nexrRingAllReduceResident), made by its first call: for every device hosting ranks
@@ -234,6 +236,16 @@ struct Prims {
   uint32_t* done = nullptr;  // the stream's completion word: [0] written by the GPU, [1] last ticket
   bool device;
   int proto = nexrRingProtoSimple;  // the communicator's, or LL for a small P2P message (sendrecv.h)
+  // Queued LL steps (enableLLAsync): a step's kernel is followed on the stream by a completion ticket,
+  // and the receive slots it consumed are released (head published) only once the ticket has landed.
+  bool llAsync = false;
+  struct PendingStep {
+    uint32_t ticket;
+    int n;
+    Conn* conn[kMaxArity];
+    uint64_t head[kMaxArity];
+  };
+  std::deque<PendingStep> pending;
 
   char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
   size_t slot(const Conn* q) const { return q->slotBytes ? q->slotBytes : c->stepBytes; }
@@ -284,6 +296,78 @@ struct Prims {
     return hipStreamSynchronize(stream) == hipSuccess;
   }
 
+  // LL steps without a host round trip per step (round 6). Host sequencing waits for every step's
+  // kernel before publishing it (streamDone), so each step costs a launch plus a wait, and the two
+  // ranks of C1 take turns: ~20 us per step. LL does not need that: its lines carry their own flags
+  // (prims_ll.h:38-93), and the kernel polls them (bounded: a flag that never comes is a timeout
+  // error, nexr_ll.hip). So a queued step publishes its send steps (incSend) as soon as its kernel is
+  // on the stream, and the receiver queues the consuming kernel at once; only the credits wait for
+  // the GPU: the slots a step read are released (postRecv, head) when its completion ticket lands
+  // (progress(), polled from every wait of this thread and by finishLL()). A kernel that polls a
+  // peer's flags must never sit in front of that peer's kernel in one hardware queue, so this is on
+  // only when the rank streams of the device fit in its hardware queues (llAsyncAllowed in
+  // nexr_ring.cpp), every rank is on one GPU (the completion word is then the step wait), and the
+  // steps run on the device.
+  void enableLLAsync() {
+    if (proto == nexrRingProtoSimple || !device || !done || !status || !c->stepWaitWord) return;
+    llAsync = true;
+    __atomic_store_n(status, 0u, __ATOMIC_RELEASE);
+  }
+  // Publishes the heads of every queued step whose ticket has landed; false (and the communicator
+  // failed) when a step's kernel reported a flag timeout.
+  bool progress() {
+    if (!llAsync) return true;
+    const uint32_t d = __atomic_load_n(done, __ATOMIC_ACQUIRE);
+    while (!pending.empty() && (int32_t)(d - pending.front().ticket) >= 0) {
+      const PendingStep& ps = pending.front();
+      for (int i = 0; i < ps.n; i++) ps.conn[i]->st->head.store(ps.head[i], std::memory_order_release);
+      pending.pop_front();
+    }
+    if (__atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) {
+      sh->fail(nexrInternalError);
+      return false;
+    }
+    return true;
+  }
+  // The end of a collective with queued steps: wait (polling, so that the heads this rank owes keep
+  // flowing to senders that still need credits) until the last step has completed.
+  bool finishLL() {
+    if (!llAsync) return true;
+    const uint32_t t = ++done[1];
+    bool landed = false;
+    if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
+      const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+      auto t0 = std::chrono::steady_clock::now();
+      for (unsigned spins = 0;; spins++) {
+        if (!progress()) {
+          llAsync = false;
+          (void)hipStreamSynchronize(stream);
+          return false;
+        }
+        if ((int32_t)(__atomic_load_n(done, __ATOMIC_ACQUIRE) - t) >= 0) {
+          landed = true;
+          break;
+        }
+        if ((spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs))
+          break;
+        if (spins >= 4096) std::this_thread::yield();
+      }
+    }
+    llAsync = false;
+    if (!landed && hipStreamSynchronize(stream) != hipSuccess) {
+      sh->fail(nexrUnhandledCudaError);
+      return false;
+    }
+    for (const PendingStep& ps : pending)  // every queued step is complete: release what it read
+      for (int i = 0; i < ps.n; i++) ps.conn[i]->st->head.store(ps.head[i], std::memory_order_release);
+    pending.clear();
+    if (__atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) {
+      sh->fail(nexrInternalError);
+      return false;
+    }
+    return true;
+  }
+
   // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
   // abortable like checkAbort (primitives.h:142-156).
   bool waitAtLeast(std::atomic<uint64_t>& a, uint64_t target) {
@@ -291,6 +375,7 @@ struct Prims {
     const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
     auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 0;; spins++) {
+      if (llAsync && !progress()) return false;
       if (a.load(std::memory_order_acquire) >= target) return true;
       if (sh->aborted()) {
         sh->fail(nexrRemoteError);
@@ -395,7 +480,7 @@ struct Prims {
       const void* src = srcBuf != kNone ? buf(srcBuf) + srcIx * esz : nullptr;
       void* dst = dstBuf != kNone ? buf(dstBuf) + dstIx * esz : nullptr;
       const int srcIsInput = srcBuf == kInput ? 1 : 0;
-      if (status) *status = 0;
+      if (status && !llAsync) *status = 0;
       const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
       nexrResult_t r;
       if (proto == nexrRingProtoLL128)
@@ -404,11 +489,38 @@ struct Prims {
       else
         r = llFn(src, srcIsInput, nr, recvLines, rf32, dst, ns, sendLines, sf32, (size_t)nelem, datatype, devOp,
                  redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
-      if (r == nexrSuccess && device && !streamDone()) r = nexrUnhandledCudaError;
-      if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
+      bool queued = false;
+      if (r == nexrSuccess && llAsync) {  // the ticket that releases this step's receive slots
+        const uint32_t t = ++done[1];
+        if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
+          PendingStep ps;
+          ps.ticket = t;
+          ps.n = nr;
+          for (int i = 0; i < nr; i++) {
+            ps.conn[i] = recv[i];
+            ps.head[i] = recv[i]->recvStep + 1;
+          }
+          pending.push_back(ps);
+          queued = true;
+        } else if (!finishLL()) {  // no ticket: wait for everything queued, then this step as before
+          return false;
+        }
+      }
+      if (!queued) {
+        if (r == nexrSuccess && device && !streamDone()) r = nexrUnhandledCudaError;
+        if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
+      }
       if (r != nexrSuccess) {
         sh->fail(r);
         return false;
+      }
+      if (queued) {  // postRecv waits for the ticket (progress); incSend publishes now
+        for (int i = 0; i < nr; i++) recv[i]->recvStep += 1;
+        for (int i = 0; i < ns; i++) {
+          send[i]->sendStep += 1;
+          send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
+        }
+        return progress();
       }
     }
     for (int i = 0; i < nr; i++) {  // postRecv (:80-83)

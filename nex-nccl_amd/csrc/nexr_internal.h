@@ -115,7 +115,7 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 #undef NEXR_DECLARE_BATCH
 
 // Workgroup geometry per (datatype, fan-in, cache policy): U packs per lane x B lanes per workgroup,
-// and whether the launch holds the kernel to one workgroup per CU (lds_for). A workgroup owns one trip
+// and how many workgroups per CU the launch admits (lds_for; 0: as the registers allow). A workgroup owns one trip
 // of U x B packs of every buffer, so the one-shot grid is nPacks / (U x B). U = 4, B = 256 is the default
 // (round-1 steady-state sweeps over U in {1,2,4,8} x B in {256,512,1024} x occupancy caps for K = 2, 4, 8:
 // profiles/r01_tune_*.log, r01_skew.log, r01s2_geom_*.log). The exceptions, each measured in one process
@@ -133,7 +133,10 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 //       K = 4-5 (every type but fp16, mixed there at K = 4): U = 1, B = 1024 — at K = 4 4.2 % faster than
 //         the two workgroups per CU its registers allow and +0.5-4 % over 4 x 256
 //         (profiles/r02_geom_sweep_*); at K = 5 3.3-3.4 % over 4 x 256 (fp32, bf16, 1.5 GiB streamed;
-//         profiles/r05zp_occupancy_k35.txt). K = 3 keeps 4 x 256: 1 x 1024 gained 2.9 % at 1 GiB with one
+//         profiles/r05zp_occupancy_k35.txt). bf16 alone takes two 512-lane workgroups per CU instead (round
+//         6, with its hardware-RNE fold): 1.4-3.2 % faster at K = 4 and 2.8 % at K = 5 on two boxes, where
+//         fp32, fp64, int32 and int8 lose 1.0-3.5 % that way (profiles/r06a_bf16cvt.txt, r06b_k45.txt).
+//         K = 3 keeps 4 x 256: 1 x 1024 gained 2.9 % at 1 GiB with one
 //         destination but lost 1.2-5.8 % at 96-300 MiB with 2-5 (profiles/r05zr_occupancy_k3m.txt), where
 //         the nt-store table of pickPolicy (nexr_api.cpp) puts those calls under this policy;
 //       K >= 6: U = 1, B = 512 — fp16 K = 8 2.5-2.7 % and fp32 K = 8 3.6 % faster than 1 x 1024, fp32
@@ -150,24 +153,46 @@ NEXR_DECLARE_BATCH(8) NEXR_DECLARE_BATCH(9)
 constexpr int kTripPacks = 1024;  // the default trip (4 x 256)
 struct Shape {
   int u, b;
-  bool oneWgPerCu;
+  int wgsPerCu;  // 0: as the registers allow; 1 or 2: held there by an LDS reservation (lds_for)
 };
 __host__ __device__ constexpr Shape shape_for(int dt, int k, int pol) {
   const bool half = dt == nexrFloat16 || dt == nexrBfloat16;
   const bool four = dt == nexrInt32 || dt == nexrUint32 || dt == nexrFloat32;
-  return (pol == 3 && k >= 6)                       ? Shape{1, 512, true}
-         : (half && k >= 8)                         ? Shape{1, 1024, false}
-         : (k == 4 && pol == 1 && !four)            ? Shape{2, 512, false}
-         : (k >= 4 && k <= 5 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, true}
-                                                    : Shape{4, 256, false};
+  return (pol == 3 && k >= 6)                       ? Shape{1, 512, 1}
+         : (half && k >= 8)                         ? Shape{1, 1024, 0}
+         : (k == 4 && pol == 1 && !four)            ? Shape{2, 512, 0}
+         : (k >= 4 && k <= 5 && pol == 3 && dt == nexrBfloat16) ? Shape{1, 512, 2}
+         : (k >= 4 && k <= 5 && pol == 3 && dt != nexrFloat16) ? Shape{1, 1024, 1}
+                                                    : Shape{4, 256, 0};
 }
 __host__ __device__ constexpr int unroll_for(int dt, int k, int pol) { return shape_for(dt, k, pol).u; }
 __host__ __device__ constexpr int block_for(int dt, int k, int pol) { return shape_for(dt, k, pol).b; }
-// One workgroup per CU: the launch reserves this many bytes of dynamic LDS (the kernel never touches
-// it), so that only one fits in a CU's 160 KiB whatever the kernel's registers would admit.
-constexpr int kLdsOneWorkgroupPerCu = 120 * 1024;
+// n workgroups per CU: the launch reserves this many bytes of dynamic LDS (the kernel never touches
+// it), so that only n fit in a CU's 160 KiB whatever the kernel's registers would admit.
+constexpr int kLdsOneWorkgroupPerCu = 120 * 1024;  // one per CU (160 / 2 < 120 <= 160)
+constexpr int kLdsTwoWorkgroupsPerCu = 66 * 1024;  // two per CU (160 / 3 < 66 <= 160 / 2)
 __host__ __device__ constexpr int lds_for(int dt, int k, int pol) {
-  return shape_for(dt, k, pol).oneWgPerCu ? kLdsOneWorkgroupPerCu : 0;
+  return shape_for(dt, k, pol).wgsPerCu == 1   ? kLdsOneWorkgroupPerCu
+         : shape_for(dt, k, pol).wgsPerCu == 2 ? kLdsTwoWorkgroupsPerCu
+                                              : 0;
 }
+
+// The reduce-copy kernels that are compiled (round 6). Every other (datatype, op, K) is routed by the
+// host onto one of them with the same bytes (routeKernel, nexr_api.cpp), so it is never launched:
+//   - K = 1 without arithmetic (no pre-op scalar, no post-op divide) is a byte copy: uint8 Sum;
+//   - signed integers' Sum, Prod, PreMulSum and SumPostDiv run the unsigned type's kernels (wrapping
+//     two's-complement arithmetic, the reference's own equivalent_primary, generate.py:128-136; the
+//     divide reads its signedness from redOpArg), so the signed objects hold Min / Max only;
+//   - PreMulSum without pre-op sources and SumPostDiv without the divide are Sum.
+// Batch launches are compiled for the plain and non-temporal-load policies only: a batch that would
+// stream enough for non-temporal stores (>= 512 MiB) runs its works as single launches, where one launch
+// per work costs nothing measurable against the work itself.
+__host__ __device__ constexpr bool is_signed_int(int dt) { return dt == nexrInt8 || dt == nexrInt32 || dt == nexrInt64; }
+__host__ __device__ constexpr bool kernel_compiled(int dt, int op, int k) {
+  return k == 1 ? (op == nexrDevSum && dt == nexrUint8) ||
+                      (!is_signed_int(dt) && (op == nexrDevPreMulSum || op == nexrDevSumPostDiv))
+                : !is_signed_int(dt) || op == nexrDevMinMax;
+}
+constexpr int kBatchPolicies = 2;  // plain (0) and non-temporal loads (1)
 
 }  // namespace nexr

@@ -216,56 +216,60 @@ static hipError_t launch_k(const RCParams& p, const Geometry& g, hipStream_t s) 
   return hipLaunchKernel(fn, dim3(g.grid), dim3(block_for(D, K, g.pol)), args, lds, s);
 }
 
+// Only the kernels kernel_compiled() names are instantiated (the host routes every other call onto
+// one of them, nexr_internal.h); asking for another is an invalid launch, never a silent fallback.
+#define NEXR_K_CASE(K, CALL) \
+  case K:                    \
+    if constexpr (kernel_compiled(D, OP, K)) return CALL; \
+    break;
+
 template <int D, int OP>
 static hipError_t launch_op(const RCParams& p, int nSrcs, const Geometry& g, hipStream_t s) {
   switch (nSrcs) {
-    case 1: return launch_k<D, OP, 1>(p, g, s);
-    case 2: return launch_k<D, OP, 2>(p, g, s);
-    case 3: return launch_k<D, OP, 3>(p, g, s);
-    case 4: return launch_k<D, OP, 4>(p, g, s);
-    case 5: return launch_k<D, OP, 5>(p, g, s);
-    case 6: return launch_k<D, OP, 6>(p, g, s);
-    case 7: return launch_k<D, OP, 7>(p, g, s);
-    case 8: return launch_k<D, OP, 8>(p, g, s);
+    NEXR_K_CASE(1, (launch_k<D, OP, 1>(p, g, s)))
+    NEXR_K_CASE(2, (launch_k<D, OP, 2>(p, g, s)))
+    NEXR_K_CASE(3, (launch_k<D, OP, 3>(p, g, s)))
+    NEXR_K_CASE(4, (launch_k<D, OP, 4>(p, g, s)))
+    NEXR_K_CASE(5, (launch_k<D, OP, 5>(p, g, s)))
+    NEXR_K_CASE(6, (launch_k<D, OP, 6>(p, g, s)))
+    NEXR_K_CASE(7, (launch_k<D, OP, 7>(p, g, s)))
+    NEXR_K_CASE(8, (launch_k<D, OP, 8>(p, g, s)))
   }
   return hipErrorInvalidValue;
 }
 
+// Batches run the plain and non-temporal-load policies only (kBatchPolicies; a batch that would stream
+// enough for non-temporal stores is run as single launches by the host), whose shapes never reserve LDS.
 template <int D, int OP, int K, bool IsMin>
 static const void* batch_kernel_for(int pol) {
-  return pol == kPolNt       ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNt, IsMin>
-         : pol == kPolNtLoad ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNtLoad, IsMin>
-                             : (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolPlain, IsMin>;
+  static_assert(lds_for(D, K, kPolPlain) == 0 && lds_for(D, K, kPolNtLoad) == 0, "batch shapes reserve no LDS");
+  return pol == kPolNtLoad ? (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolNtLoad, IsMin>
+                           : (const void*)&reduce_copy_batch_kernel<D, OP, K, kPolPlain, IsMin>;
 }
 
 // Every work of a MinMax batch has the same isMin (reduceCopyBatch groups them so).
 template <int D, int OP, int K>
 static hipError_t launch_batch_k(const BatchParams& b, int pol, int grid, hipStream_t s) {
+  if (pol != kPolPlain && pol != kPolNtLoad) return hipErrorInvalidValue;
   const void* fn = batch_kernel_for<D, OP, K, false>(pol);
   if constexpr (OP == nexrDevMinMax) {
     if ((b.w[0].redArg & 1) == 0) fn = batch_kernel_for<D, OP, K, true>(pol);
   }
-  const int lds = lds_for(D, K, pol);
-  if (lds > 64 * 1024) {
-    static std::atomic<uint64_t> allowed[2][4];
-    const hipError_t e = allow_lds(fn, lds, allowed[fn == batch_kernel_for<D, OP, K, false>(pol) ? 0 : 1][pol & 3], s);
-    if (e != hipSuccess) return e;
-  }
   void* args[] = {const_cast<BatchParams*>(&b)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(block_for(D, K, pol)), args, lds, s);
+  return hipLaunchKernel(fn, dim3(grid), dim3(block_for(D, K, pol)), args, 0, s);
 }
 
 template <int D, int OP>
 static hipError_t launch_batch_op(const BatchParams& b, int nSrcs, int pol, int grid, hipStream_t s) {
   switch (nSrcs) {
-    case 1: return launch_batch_k<D, OP, 1>(b, pol, grid, s);
-    case 2: return launch_batch_k<D, OP, 2>(b, pol, grid, s);
-    case 3: return launch_batch_k<D, OP, 3>(b, pol, grid, s);
-    case 4: return launch_batch_k<D, OP, 4>(b, pol, grid, s);
-    case 5: return launch_batch_k<D, OP, 5>(b, pol, grid, s);
-    case 6: return launch_batch_k<D, OP, 6>(b, pol, grid, s);
-    case 7: return launch_batch_k<D, OP, 7>(b, pol, grid, s);
-    case 8: return launch_batch_k<D, OP, 8>(b, pol, grid, s);
+    NEXR_K_CASE(1, (launch_batch_k<D, OP, 1>(b, pol, grid, s)))
+    NEXR_K_CASE(2, (launch_batch_k<D, OP, 2>(b, pol, grid, s)))
+    NEXR_K_CASE(3, (launch_batch_k<D, OP, 3>(b, pol, grid, s)))
+    NEXR_K_CASE(4, (launch_batch_k<D, OP, 4>(b, pol, grid, s)))
+    NEXR_K_CASE(5, (launch_batch_k<D, OP, 5>(b, pol, grid, s)))
+    NEXR_K_CASE(6, (launch_batch_k<D, OP, 6>(b, pol, grid, s)))
+    NEXR_K_CASE(7, (launch_batch_k<D, OP, 7>(b, pol, grid, s)))
+    NEXR_K_CASE(8, (launch_batch_k<D, OP, 8>(b, pol, grid, s)))
   }
   return hipErrorInvalidValue;
 }

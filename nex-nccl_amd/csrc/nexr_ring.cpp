@@ -544,6 +544,40 @@ bool validConfigBuff(const nexrRingComm* c) {
          (c->proto != nexrRingProtoLL128 || c->cfg.buffBytes % (kSteps * 2048) == 0);  // whole LL128 slices
 }
 
+// Queued LL steps (Prims::enableLLAsync) for thread ranks: a kernel that polls its peer's line flags
+// must never wait behind that peer's kernel in one hardware queue, so they are on only when every rank
+// stream of the device (all channels, the tree's second streams included) can have a hardware queue of
+// its own beside the default stream's: at most GPU_MAX_HW_QUEUES - 1 of them (HIP's default is 4
+// queues per device; beyond that streams share queues). Every rank on one GPU and FIFOs in device
+// memory, as enableLLAsync requires. NEXR_LL_ASYNC=0 keeps host sequencing, =1 skips the queue count.
+bool llAsyncAllowed(const nexrRingComm* c) {
+  static const int forced = [] {
+    const char* e = getenv("NEXR_LL_ASYNC");
+    return e && *e ? (e[0] == '0' ? 0 : 1) : -1;
+  }();
+  static const long hwQueues = [] {
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    const long v = e && *e ? strtol(e, nullptr, 10) : 4;
+    return v > 0 ? v : 4;
+  }();
+  if (forced == 0 || !c->ll || !c->stepWaitWord || c->cfg.memMode != nexrRingDeviceMemory) return false;
+  if (forced == 1) return true;
+  std::vector<std::pair<int, int>> perDev;  // (device, rank streams on it)
+  const int nCh = 1 + (int)c->channels.size();
+  for (int k = 0; k < nCh; k++) {
+    const nexrRingComm* ck = k == 0 ? c : c->channels[(size_t)k - 1];
+    for (size_t r = 0; r < ck->streams.size(); r++) {
+      const int streams = (ck->streams[r] ? 1 : 0) + (r < ck->streams2.size() && ck->streams2[r] ? 1 : 0);
+      auto it = std::find_if(perDev.begin(), perDev.end(), [&](const std::pair<int, int>& x) { return x.first == ck->devices[r]; });
+      if (it == perDev.end()) perDev.emplace_back(ck->devices[r], streams);
+      else it->second += streams;
+    }
+  }
+  for (const auto& d : perDev)
+    if (d.second > hwQueues - 1) return false;
+  return true;
+}
+
 // Thread-rank collectives: the ring schedules on one thread per rank.
 nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* sendbuffs, void* const* recvbuffs,
                             size_t count, int datatype, int op, int root) {
@@ -567,6 +601,8 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
   std::vector<ChannelPart> parts = channelParts(c, (int64_t)count, esz, trafficPerByte);
   for (ChannelPart& part : parts) part.chunkCount = chunkElems(channelComm(c, part.channel), g, esz, false, 0);
   Shared sh;
+  const bool llAsync = llAsyncAllowed(c);
+  c->lastLLAsync = llAsync;
   std::vector<std::function<void()>> jobs;
   for (const ChannelPart& part : parts) {
     for (int rank = 0; rank < n; rank++) {
@@ -578,6 +614,7 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
         p.recv[p.nRecv++] = ck->conns[rank];
         p.send[p.nSend++] = ck->conns[(rank + 1) % n];
         p.attach();
+        if (llAsync) p.enableLLAsync();
         switch (coll) {
           case kAllReduce: runRingAllReduce(p, n, part); break;
           case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count, part); break;
@@ -585,6 +622,7 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
           case kReduce: runRingReduce(p, n, root, part); break;
           case kBroadcast: runRingBroadcast(p, n, root, part); break;
         }
+        p.finishLL();  // queued LL steps complete before the collective returns (even after a failure)
       });
     }
   }
@@ -911,6 +949,12 @@ NEXR_API nexrResult_t nexrTreeAllReduce(nexrRingComm_t c, const void* const* sen
 NEXR_API nexrResult_t nexrRingCommGetStepWait(nexrRingComm_t c, int* word) {
   if (!c || !word) return nexrInvalidArgument;
   *word = c->stepWaitWord ? 1 : 0;
+  return nexrSuccess;
+}
+
+NEXR_API nexrResult_t nexrRingCommGetLLQueued(nexrRingComm_t c, int* queued) {
+  if (!c || !queued) return nexrInvalidArgument;
+  *queued = c->lastLLAsync ? 1 : 0;
   return nexrSuccess;
 }
 

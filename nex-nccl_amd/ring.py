@@ -20,7 +20,7 @@ RING_LIB_PATH = os.path.join(_HERE, "libnexr_ring.so")
 EXTRAS_LIB_PATH = os.path.join(_HERE, "libnexr_extras.so")
 RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceScatter", "nexrRingAllGather",
                     "nexrRingReduce", "nexrRingBroadcast", "nexrTreeAllReduce", "nexrTreeTopology",
-                    "nexrRingCommGetStepWait", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
+                    "nexrRingCommGetStepWait", "nexrRingCommGetLLQueued", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
                     "nexrPeerRingAllReduce", "nexrPeerRingReduceScatter", "nexrPeerRingAllGather",
                     "nexrPeerRingReduce", "nexrPeerRingBroadcast")
 EXTRAS_ABI_SYMBOLS = ("nexrSendRecv", "nexrPeerSendRecv", "nexrRingAllReduceResident",
@@ -68,6 +68,7 @@ def _bind_ring(L: ctypes.CDLL) -> None:
         getattr(L, name).argtypes = [vp, vp, vp, sz, i32] + extra
     L.nexrTreeTopology.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.nexrRingCommGetStepWait.argtypes = [vp, ctypes.POINTER(i32)]
+    L.nexrRingCommGetLLQueued.argtypes = [vp, ctypes.POINTER(i32)]
     L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
     L.nexrRingCommDestroy.argtypes = [vp]
     for name in RING_ABI_SYMBOLS:
@@ -220,6 +221,13 @@ class RingComm:
         w = ctypes.c_int()
         _check(self._L.nexrRingCommGetStepWait(self._h, ctypes.byref(w)), "nexrRingCommGetStepWait")
         return "word" if w.value else "sync"
+
+    def ll_queued(self) -> bool:
+        """Whether the last ring collective queued its LL / LL128 steps without a host wait per step
+        (nexrRingCommGetLLQueued)."""
+        w = ctypes.c_int()
+        _check(self._L.nexrRingCommGetLLQueued(self._h, ctypes.byref(w)), "nexrRingCommGetLLQueued")
+        return bool(w.value)
 
     def tree_topology(self, rank: int):
         """(up, [down...]) of `rank` in this communicator's tree (-1 = none)."""

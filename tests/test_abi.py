@@ -204,12 +204,13 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
     assert (info.grid, info.block, info.packsPerLane, info.policy) == (16384, 256, 4, 3)
     # K = 4: the geometry follows the cache policy (nexr_internal.h shape_for): C4 (64 MiB per
     # buffer, 320 MiB streamed: nt loads) runs 2 packs x 512 lanes for 1-, 2- and 8-byte types and the
-    # default 4 x 256 for 4-byte ones; >= 512 MiB streamed (nt loads and stores) 1 x 1024, except fp16;
+    # default 4 x 256 for 4-byte ones; >= 512 MiB streamed (nt loads and stores) 1 x 1024, except fp16
+    # (4 x 256) and bf16 (1 x 512, two per CU: round 6);
     # below 64 MiB streamed the default 4 x 256.
     k4 = [0x10000000 * (i + 1) for i in range(4)]
     for dt, n, want in ((2, 16 << 20, (4096, 256, 4, 1)), (0, 64 << 20, (4096, 512, 2, 1)),
                         (9, 32 << 20, (4096, 512, 2, 1)), (7, 16 << 20, (4096, 256, 4, 1)),
-                        (2, 64 << 20, (16384, 1024, 1, 3)), (9, 128 << 20, (16384, 1024, 1, 3)),
+                        (2, 64 << 20, (16384, 1024, 1, 3)), (9, 128 << 20, (32768, 512, 1, 3)),
                         (6, 128 << 20, (16384, 256, 4, 3)), (2, 1 << 20, (256, 256, 4, 0))):
         info = nexr.query_launch(k4, [0x60000000], n, dt)
         assert (info.grid, info.block, info.packsPerLane, info.policy) == want, (dt, n)

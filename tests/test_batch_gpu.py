@@ -324,3 +324,29 @@ def test_multi_device_c5_eight_chunks_folded_onto_one_call(nexr, dev):
             assert torch.equal(o.view(torch.int32), (a + b).view(torch.int32)), f"work {w} on GPU {d}"
     del bufs
     torch.cuda.empty_cache()
+
+
+def test_batch_past_the_nt_store_threshold_runs_single_launches(nexr, oracle, dev):
+    """Round 6: batch kernels are compiled for the plain and nt-load policies only; a run of works that
+    streams >= 512 MiB (where a single launch would take nt stores) is launched work by work, each at
+    its own policy. Two 104 MiB works and a small one of the same (datatype, op, K): 632 MiB streamed,
+    all exact, with a K = 1 copy and a signed-integer Sum batch beside them (routed kernels)."""
+    rng = np.random.default_rng(31)
+    works = [
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 2, 1, 26 << 20, 1, rng, "zero"),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 2, 1, 5_000, 2, rng, "phase"),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 2, 1, 26 << 20, 3, rng, "random"),
+        _Work(nexr, oracle, mg.F32, mg.SUM, "sum", 1, 2, 1_000_003, 4, rng, "phase"),
+    ]
+    nexr.reduce_copy_batch([w.work for w in works], mg.F32, mg.SUM)
+    torch.cuda.synchronize()
+    for i, w in enumerate(works):
+        w.check(("nt-store run", i))
+    del works
+    torch.cuda.empty_cache()
+    for op, name in ((mg.SUM, "sum"), (mg.PROD, "prod")):
+        sub = [_Work(nexr, oracle, mg.I32, op, name, k, 1, 70_001 + k, 10 + k, rng, "random") for k in (1, 2, 3)]
+        nexr.reduce_copy_batch([w.work for w in sub], mg.I32, op)
+        torch.cuda.synchronize()
+        for i, w in enumerate(sub):
+            w.check(("int32 routed", name, i))

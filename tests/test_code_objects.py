@@ -9,6 +9,7 @@ AMDGPU metadata note, that ``.symtab`` holds both the kernel's symbol and its ``
 build a one-kernel object both ways to show the check tells the two links apart.
 """
 import os
+import re
 import shutil
 import struct
 import subprocess
@@ -139,3 +140,56 @@ def test_makefile_links_device_code_with_discard_all():
     kflags = [l for l in mk.splitlines() if l.startswith("KFLAGS")]
     assert kflags and "--discard-all" in kflags[0] and "--strip-all" not in kflags[0]
     assert shutil.which("make") is not None
+
+
+# ---- which reduce-copy kernels are compiled (round 6: routing instead of every combination) ----------
+SUM, PROD, MINMAX, PREMULSUM, SUMPOSTDIV = range(5)
+INT8, UINT8, INT32, UINT32, INT64, UINT64, F16, F32, F64, BF16 = range(10)
+_SIGNED = {INT8, INT32, INT64}
+_INTS = {INT8, UINT8, INT32, UINT32, INT64, UINT64}
+
+
+def expected_kernels():
+    """(batch, dt, op, K, policy, isMin) of every kernel the routing (nexr_api.cpp routeKernel,
+    nexr_internal.h kernel_compiled) can launch: K = 1 without arithmetic runs the uint8 Sum copy,
+    signed integers run only Min / Max (Sum, Prod, PreMulSum, SumPostDiv on the unsigned kernels), batch
+    launches run the plain and nt-load policies only."""
+    out = set()
+    for dt in range(10):
+        for op in range(5):
+            if op == SUMPOSTDIV and dt not in _INTS:
+                continue
+            for k in range(1, 9):
+                if k == 1:
+                    ok = (op == SUM and dt == UINT8) or (dt not in _SIGNED and op in (PREMULSUM, SUMPOSTDIV))
+                else:
+                    ok = dt not in _SIGNED or op == MINMAX
+                if not ok:
+                    continue
+                for batch, pols in ((0, (0, 1, 3)), (1, (0, 1))):
+                    for pol in pols:
+                        for is_min in ((0, 1) if op == MINMAX else (0,)):
+                            out.add((batch, dt, op, k, pol, is_min))
+    return out
+
+
+_KNAME = re.compile(r"_ZN4nexr(18reduce_copy_kernel|24reduce_copy_batch_kernel)ILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])")
+
+
+def test_compiled_reduce_copy_kernels_are_exactly_the_routed_set():
+    path = os.path.join(PKG, "libnexr.so")
+    if not os.path.exists(path):
+        pytest.skip("libnexr.so not built")
+    got = set()
+    for co in gfx950_code_objects(_read(path)):
+        _tables, notes = elf_tables(co)
+        for k in (k for n in notes for k in n["amdhsa.kernels"]):
+            m = _KNAME.match(k[".name"])
+            if m:
+                key = (int("batch" in m.group(1)), int(m.group(2)), int(m.group(3)), int(m.group(4)),
+                       int(m.group(5)), int(m.group(6)))
+                assert key not in got, key
+                got.add(key)
+    want = expected_kernels()
+    assert got == want, (sorted(got - want)[:5], sorted(want - got)[:5])
+    assert len(want) == 1595  # 2,688 before round 6 (every dt x op x K x policy x {single, batch})

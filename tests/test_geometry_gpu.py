@@ -78,7 +78,7 @@ MIB = 1 << 20
 
 @pytest.mark.parametrize("dt,op,name,buf_mib", [
     (mg.I8, mg.MINMAX, "min", 16), (mg.I32, mg.PROD, "prod", 16), (mg.F32, mg.SUM, "sum", 13),  # 2 x 512 / 4 x 256
-    (mg.U32, mg.MINMAX, "max", 104), (mg.BF16, mg.SUM, "sum", 104),                              # 1 x 1024
+    (mg.U32, mg.MINMAX, "max", 104), (mg.BF16, mg.SUM, "sum", 104),                              # 1 x 1024 / 2 x 512
     (mg.F16, mg.SUM, "sum", 104)])                                                               # 4 x 256
 def test_k4_policy_geometries_edges(nexr, oracle, dev, dt, op, name, buf_mib):
     esz = np.dtype(mg.STORE[dt]).itemsize
@@ -93,7 +93,7 @@ def test_k4_policy_geometries_edges(nexr, oracle, dev, dt, op, name, buf_mib):
             if info.policy == 1:
                 assert info.block == (256 if esz == 4 else 512)
             else:
-                assert info.block == (256 if dt == mg.F16 else 1024)
+                assert info.block == {mg.F16: 256, mg.BF16: 512}.get(dt, 1024)
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
         got = _run(nexr, srcs, dt, op, arg, offs)
         assert mg.canon_bytes(dt, got) == mg.canon_bytes(dt, exp), (n, offs)

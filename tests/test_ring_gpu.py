@@ -134,3 +134,61 @@ def test_step_wait_modes_give_the_same_results(wait):
     assert d["ok"]
     expect = wait if wait != "default" else ("word" if d["n_vis"] == 1 else "sync")
     assert d["waits"] == [expect], d
+
+
+@pytest.mark.parametrize("proto", ["ll", "ll128"])
+@pytest.mark.parametrize("n_ranks", [2, 3, 4])
+def test_ll_ring_queued_steps(ring, oracle, proto, n_ranks):
+    """Round 6: LL / LL128 ring steps queued on each rank's stream with no host wait per step (the
+    kernel finds the peer's data by its line flags; a step's receive slots are released when its
+    completion ticket lands). On one GPU they queue while the rank streams fit beside the default
+    stream in HIP's 4 hardware queues (2 and 3 ranks), and 4 ranks fall back to host sequencing. Three
+    calls in a row on one communicator (the step counters and flags carry over), every rank exact
+    against the oracle's LL fold order."""
+    from oracle.ring import ring_allreduce_expected_ll
+    dt, op = (mg.F32, 0) if proto == "ll" else (mg.BF16, 0)
+    count = 600_007
+    p = ring.PROTO_LL if proto == "ll" else ring.PROTO_LL128
+    with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, 0, None, 20000, p) as comm:
+        for call in range(3):
+            inputs = mg.gen_inputs(dt, n_ranks, count, 700 + 13 * call + n_ranks, special=True)
+            send = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+            recv = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.all_reduce([s.data_ptr() for s in send], [d.data_ptr() for d in recv], count, dt, op)
+            exp = (ring_allreduce_expected_ll(inputs, dt, op) if proto == "ll"
+                   else ring_allreduce_expected_ll(inputs, dt, op, 120 * 640 * 8 * 8, proto="ll128"))
+            for r in range(n_ranks):
+                assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), (call, r)
+            one_gpu = torch.cuda.device_count() == 1
+            assert comm.ll_queued() == (one_gpu and n_ranks <= 3), (comm.ll_queued(), n_ranks)
+
+
+def test_ll_ring_queued_off_by_env():
+    """NEXR_LL_ASYNC=0 (read once per process) keeps host-sequenced LL steps: same exact sums, and the
+    communicator reports that it did not queue."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = r"""
+import importlib, json, sys
+sys.path.insert(0, {root!r})
+import numpy as np, torch
+ring = importlib.import_module("nex-nccl_amd.ring")
+rng = np.random.default_rng(8)
+x = [rng.integers(-1000, 1000, 300_001).astype(np.float32) for _ in range(2)]
+send = [torch.from_numpy(v).cuda() for v in x]
+recv = [torch.zeros_like(t) for t in send]
+torch.cuda.synchronize()
+with ring.RingComm(2, ring.DEVICE_MEMORY, 0, protocol=ring.PROTO_LL) as comm:
+    comm.all_reduce([t.data_ptr() for t in send], [t.data_ptr() for t in recv], 300_001, 7, 0)
+    q = comm.ll_queued()
+print(json.dumps({{"ok": all(np.array_equal(r.cpu().numpy(), x[0] + x[1]) for r in recv), "queued": q}}))
+""".format(root=root)
+    env = dict(os.environ, NEXR_LL_ASYNC="0")
+    out = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d == {"ok": True, "queued": False}, d

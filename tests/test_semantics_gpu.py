@@ -65,7 +65,7 @@ def test_in_place_host_staged_and_one_rank(nexr, oracle, dev, mode):
 def test_batch(nexr, oracle, dt, dev, mode):
     batch_t.test_batch_mixed_works_match_oracle(nexr, oracle, dt, dev)
     if dt == mg.I8:
-        batch_t.test_batch_min_and_max_in_one_launch(nexr, oracle, dev)
+        batch_t.test_batch_min_and_max_in_one_call(nexr, oracle, dev)
 
 
 @pytest.mark.parametrize("dt", [mg.I8, mg.I32, mg.I64, mg.F16, mg.BF16, mg.F32])

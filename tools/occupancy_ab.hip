@@ -90,6 +90,7 @@ struct Var {
   int trip;  // packs per workgroup trip (U x B)
   uint64_t redArg;
   int k;  // the fan-in the kernel was compiled for: must equal the configuration's source count
+  unsigned grid = 0;  // workgroups of the launch (0: one-shot, one per trip); fewer: the kernel grid-strides
 };
 struct Cfg {
   const char* name;
@@ -427,6 +428,34 @@ int main(int argc, char** argv) {
                     {var<D, OP, K4, P, false, 1, 1024>("hw U1 B1024", 1), var<D, OP, K4, P, false, 1, 512>("hw U1 B512", 2),
                      var<D0, OP, K4, P, false, 1, 1024>("int U1 B1024", 1)}});
   }
+  if (group == "c4grid") {  // round 6: C4's ~3.6 us per launch inside the kernel: one-shot grid vs a grid-strided one
+    constexpr int K = 4, P = kPolNtLoad;
+    auto capped = [](Var v, unsigned grid) {
+      v.grid = grid;
+      v.name += ", grid " + std::to_string(grid);
+      return v;
+    };
+    {
+      constexpr int D = nexrInt32, OP = nexrDevMinMax;
+      const Var one = var<D, OP, K, P, true, 4, 256>("U4 B256", 0, 0x80000000ull);
+      cfgs.push_back({"C4 int32 min K=4 64 MiB (nt loads): one-shot 4096 workgroups vs grid-strided", K, 64u << 20, all,
+                      {one, capped(one, 2048), capped(one, 1024), capped(one, 3072), var<D, OP, K, P, true, 2, 256>("U2 B256", 0, 0x80000000ull),
+                       var<D, OP, K, P, true, 8, 256>("U8 B256", 0, 0x80000000ull)}});
+    }
+    {
+      constexpr int D = nexrInt8, OP = nexrDevMinMax;
+      const Var one = var<D, OP, K, P, false, 2, 512>("U2 B512", 0, 0x7f);
+      cfgs.push_back({"C4 int8 max K=4 64 MiB (nt loads): one-shot 4096 workgroups vs grid-strided", K, 64u << 20, all,
+                      {one, capped(one, 1024), capped(one, 512), capped(one, 2048), var<D, OP, K, P, false, 1, 512>("U1 B512", 0, 0x7f),
+                       var<D, OP, K, P, false, 4, 512>("U4 B512", 0, 0x7f)}});
+    }
+    {
+      constexpr int D = nexrFloat32, OP = nexrDevSum, K2 = 2;
+      const Var one = var<D, OP, K2, kPolNt, false, 4, 256>("U4 B256", 0);
+      cfgs.push_back({"C2 fp32 sum K=2 256 MiB (nt/nt): one-shot 16384 workgroups vs grid-strided", K2, 256u << 20, fin,
+                      {one, capped(one, 2048), capped(one, 4096), capped(one, 8192)}});
+    }
+  }
   if (group == "k45") {  // round 6: K = 4-5 under nt stores, 1 x 1024 at one per CU (production) vs 1 x 512 at two
     constexpr int P = kPolNt;
 #define K45(D, OP, K, ISMIN, ARG, NAME, MASK)                                                                \
@@ -535,7 +564,8 @@ int main(int argc, char** argv) {
       const Var& v = cf.vars[vi];
       RCParams p = params(v, r);
       void* args[] = {&p};
-      CK(hipLaunchKernel(v.fn, dim3((unsigned)(cf.bytes / 16 / v.trip)), dim3(v.block), args, lds_for(v.wgs), nullptr));
+      const unsigned grid = v.grid ? v.grid : (unsigned)(cf.bytes / 16 / v.trip);
+      CK(hipLaunchKernel(v.fn, dim3(grid), dim3(v.block), args, lds_for(v.wgs), nullptr));
     };
     printf("%s\n", cf.name);
     {  // bytes of every variant against the first (production) launch, set 0
