@@ -206,12 +206,12 @@ NEXR_API nexrResult_t nexrReduceCopyHost(int nSrcs, const void* const* srcs, int
  * (src/nccl.h.in:130-133, src/allocator.cc) for the fork's setting, where NEX "device memory" and
  * the transport's staging FIFOs are host memory.
  *   nexrHostRegister    page-locks and device-maps [buff, buff + size) (hipHostRegister, mapped +
- *                       portable) and records the pages it touches in a process-wide cache sorted by
- *                       address, like the reference's regCache (register.cc:40-60). A range inside the
- *                       pages of an entry already here (registered, or from nexrHostMemAlloc) shares
- *                       that entry (one more reference); a range that reaches into an entry's pages
- *                       without lying inside them returns nexrInvalidUsage. *handle is an opaque id
- *                       that is never reused.
+ *                       portable) and records it in a process-wide cache sorted by address, like the
+ *                       reference's regCache (register.cc:40-60). A range inside an entry already here
+ *                       (registered, or from nexrHostMemAlloc) shares that entry (one more reference);
+ *                       a range that partly overlaps one returns nexrInvalidUsage. Disjoint ranges that
+ *                       share a page are separate entries (the runtime maps each; if it refused one,
+ *                       nexrInvalidUsage). *handle is an opaque id that is never reused.
  *   nexrHostDeregister  drops one reference; the last one unregisters the range (NULL: no-op). A
  *                       handle with no reference left, or never issued, returns nexrInvalidUsage.
  *   nexrHostMemAlloc    pinned, device-mapped host memory (hipHostMalloc), recorded in the same cache.

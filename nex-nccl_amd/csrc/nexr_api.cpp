@@ -935,13 +935,15 @@ uint16_t floatToBf16Rne(float f) {
 // (nexrHostMemAlloc), sorted by begin address. nexrReduceCopyHost looks a buffer up here first, so a
 // call on registered memory costs no HIP query per buffer; because the library made every entry, it
 // also knows when one ends (nexrHostDeregister / nexrHostMemFree), so nothing here goes stale.
-// Entries cover whole pages: hipHostRegister pins and maps every page the range touches, so two
-// buffers that share a page share one entry (the second registration is one more reference), and a
-// range that reaches into an entry's pages without lying inside them is refused (nexrInvalidUsage)
-// instead of failing in the runtime. Handles are monotonic ids, never addresses: a handle whose
-// entry is gone stays invalid even when a later entry lands at the same address.
+// Entries hold exact byte ranges. hipHostRegister pins every page a range touches, and on this ROCm it
+// accepts a second range that shares a page with a registered one (adjacent heap buffers do, e.g. the
+// C1 bench's numpy arrays), giving it a mapping of its own, so such neighbours are separate entries
+// whose deregistrations are independent (tests/test_host_register_gpu.py); should the runtime refuse
+// one, the call returns nexrInvalidUsage, not a raw HIP error. Handles are monotonic ids, never
+// addresses: a handle whose entry is gone stays invalid even when a later entry lands at the same
+// address.
 struct HostReg {
-  uintptr_t beg = 0, end = 0;  // the pages: [page floor of the first byte, page end of the last)
+  uintptr_t beg = 0, end = 0;
   char* dev = nullptr;         // device address of beg
   void* hipPtr = nullptr;      // the pointer hipHostRegister / hipHostMalloc returned or took
   bool owned = false;          // allocated by nexrHostMemAlloc (freed by nexrHostMemFree), else registered
@@ -974,15 +976,16 @@ bool regLookup(const void* p, size_t bytes, void** dev) {
   return true;
 }
 
-// Index of the entry whose pages contain [a, a + n), -1 if none; overlap: some entry's pages
-// intersect the range's pages.
-int regFind(uintptr_t a, size_t n, bool* overlap) {
-  *overlap = false;
+// Index of the entry containing [a, a + n), -1 if none; overlap: some entry intersects it; sharesPage:
+// some entry shares a page with it.
+int regFind(uintptr_t a, size_t n, bool* overlap, bool* sharesPage) {
+  *overlap = *sharesPage = false;
   const uintptr_t pb = pageFloor(a), pe = pageCeil(a + n);
   for (size_t i = 0; i < gRegs.size(); i++) {
     const HostReg* r = gRegs[i];
     if (a >= r->beg && a + n <= r->end) return (int)i;
-    if (pb < r->end && pe > r->beg) *overlap = true;
+    if (a < r->end && a + n > r->beg) *overlap = true;
+    if (pb < pageCeil(r->end) && pe > pageFloor(r->beg)) *sharesPage = true;
   }
   return -1;
 }
@@ -1217,25 +1220,32 @@ NEXR_API nexrResult_t nexrHostRegister(void* buff, size_t size, void** handle) {
   const uintptr_t a = (uintptr_t)buff;
   if (a + size < a) return nexrInvalidArgument;
   std::unique_lock<std::shared_mutex> lk(gRegMu);
-  bool overlap = false;
-  const int i = regFind(a, size, &overlap);
-  if (i >= 0) {  // inside pages this library already maps (registered or allocated): share them (register.cc:49-76)
+  bool overlap = false, sharesPage = false;
+  const int i = regFind(a, size, &overlap, &sharesPage);
+  if (i >= 0) {  // inside a range this library already maps (registered or allocated): share it (register.cc:49-76)
     gRegs[i]->regs++;
     *handle = (void*)(uintptr_t)gRegs[i]->id;
     return nexrSuccess;
   }
-  if (overlap) return nexrInvalidUsage;  // reaches into another entry's pages: hipHostRegister would refuse it
-  NEXR_HIP(hipHostRegister(buff, size, hipHostRegisterMapped | hipHostRegisterPortable));
+  if (overlap) return nexrInvalidUsage;  // partly inside another entry: hipHostRegister would refuse it
+  hipError_t e = hipHostRegister(buff, size, hipHostRegisterMapped | hipHostRegisterPortable);
+  if (e != hipSuccess) {
+    if (sharesPage) {  // a page-sharing neighbour the runtime refused: the documented usage error
+      (void)hipGetLastError();
+      return nexrInvalidUsage;
+    }
+    return hipFail(e);
+  }
   void* dev = nullptr;
-  hipError_t e = hipHostGetDevicePointer(&dev, buff, 0);
+  e = hipHostGetDevicePointer(&dev, buff, 0);
   if (e != hipSuccess) {
     (void)hipHostUnregister(buff);
     return hipFail(e);
   }
   HostReg* r = new HostReg();
-  r->beg = pageFloor(a);
-  r->end = pageCeil(a + size);
-  r->dev = (char*)dev - (a - r->beg);  // the mapping covers whole pages
+  r->beg = a;
+  r->end = a + size;
+  r->dev = (char*)dev;
   r->hipPtr = buff;
   r->regs = 1;
   regInsert(r);
@@ -1269,9 +1279,9 @@ NEXR_API nexrResult_t nexrHostMemAlloc(void** ptr, size_t size) {
     return hipFail(e);
   }
   HostReg* r = new HostReg();
-  r->beg = pageFloor((uintptr_t)host);
-  r->end = pageCeil((uintptr_t)host + size);
-  r->dev = (char*)dev - ((uintptr_t)host - r->beg);
+  r->beg = (uintptr_t)host;
+  r->end = (uintptr_t)host + size;
+  r->dev = (char*)dev;
   r->hipPtr = host;
   r->owned = true;
   std::unique_lock<std::shared_mutex> lk(gRegMu);

@@ -40,6 +40,7 @@ def test_bench_extra_configs_and_c1():
                                        "c4_i8_max", "c4_i8_prod"}
     for v in d["extra_configs"].values():
         assert 0 < v["frac"] < 1
+    assert "error" not in d["c1_ring"], d["c1_ring"]
     assert all(d["c1_ring"][k]["exact"] for k in ("device", "device_ll", "device_ll128", "host_staged", "cpu_oracle"))
     assert d["c1_ring"]["device"]["step_wait"] == "word"  # both emulated ranks on the one GPU
     assert "resident_ring" not in d and "device_resident" not in d["c1_ring"]  # extras: not in the default line

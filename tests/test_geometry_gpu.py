@@ -231,14 +231,15 @@ def test_small_fan_in_nt_store_policy_edges(nexr, oracle, dev, dt, k, m, op, nam
                                                   (mg.I8, 5, mg.MINMAX, "min", 88)])
 def test_k5_nt_store_geometry_edges(nexr, oracle, dev, dt, k, op, name, buf_mib):
     """K = 5 under the nt-store policy runs one pack x 1024 lanes at one workgroup per CU, as K = 4 does
-    (round 5); whole trips, a remainder plus edges, and mixed phases against the oracle."""
+    (round 5), and bf16 one pack x 512 lanes at two per CU (round 6); whole trips, a remainder plus
+    edges, and mixed phases against the oracle."""
     esz = np.dtype(mg.STORE[dt]).itemsize
     base = buf_mib * MIB // esz
     arg = mg.minmax_arg(dt, name == "max") if op == mg.MINMAX else 0
     for n, offs in ((base, None), (base + 16 // esz * 1024 * 3 + 5, None), (base - 7, [esz * (i % 2) for i in range(k + 1)])):
         info = nexr.query_launch([0x1000000 * (i + 1) + (offs[i] if offs else 0) for i in range(k)],
                                  [0x90000000 + (offs[k] if offs else 0)], n, dt)
-        assert (info.policy, info.block, info.packsPerLane) == (3, 1024, 1), (n, offs)
+        assert (info.policy, info.block, info.packsPerLane) == (3, 512 if dt == mg.BF16 else 1024, 1), (n, offs)
         srcs = mg.gen_inputs(dt, k, n, 5300 + n % 1013, special=True)
         exp = oracle.reduce_copy(srcs, 1, dt, op, arg, threads=16)[0]
         got = _run(nexr, srcs, dt, op, arg, offs)

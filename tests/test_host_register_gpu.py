@@ -271,47 +271,43 @@ def test_register_inside_an_allocation_then_free(hip):
     assert e.value.code == 5
 
 
-def test_sub_page_neighbours_share_one_entry(hip):
-    """Advisor r5 (low): hipHostRegister pins whole pages, so two disjoint buffers in one page cannot be
-    registered twice with the runtime. The second registration shares the first one's entry (one
-    handle, two references), a call on the second buffer is read in place from the cache, and only the
-    last deregistration unpins the page. A range reaching into the entry's pages from outside is
-    refused with nexrInvalidUsage, not a raw HIP error."""
+def test_sub_page_neighbours_register_separately(hip):
+    """Advisor r5 (low): hipHostRegister pins whole pages, so two disjoint buffers in one page (adjacent
+    heap blocks, as the C1 bench's numpy arrays are) both touch the same page. On this ROCm the runtime
+    maps each registration separately: two entries, two handles, each buffer read in place from the
+    cache, and deregistering one leaves the other's mapping working. A range that overlaps an entry's
+    bytes is refused with nexrInvalidUsage."""
     nexr = importlib.import_module("nex-nccl_amd")
     reg = Region(hip, 4 * 4096, register=False)
     n = 100
+    a_off, out_off = 4096 + 2048, 4096 + 16  # a and b share page 1 with out
     try:
-        ha = nexr.host_register(reg.base + 4096 + 16, 4 * n)       # buffer A in page 1
-        hb = nexr.host_register(reg.base + 4096 + 2048, 8 * n)     # buffer B, same page, disjoint
-        assert ha == hb
-        with pytest.raises(nexr.NexrError) as e:  # from page 0 into page 1
-            nexr.host_register(reg.base + 4000, 200)
+        hs = nexr.host_register(reg.base + a_off, 8 * n)      # a and b: one range
+        ho = nexr.host_register(reg.base + out_off, 4 * n)    # out: same page, disjoint bytes
+        assert hs != ho
+        with pytest.raises(nexr.NexrError) as e:  # overlaps out's bytes
+            nexr.host_register(reg.base + out_off + 8, 4 * n)
         assert e.value.code == 5
-        a = reg.f32(4096 + 2048, n)
-        b = reg.f32(4096 + 2048 + 4 * n, n)
-        out = reg.f32(4096 + 16, n)  # A's bytes: same page, read in place too
+        a = reg.f32(a_off, n)
+        b = reg.f32(a_off + 4 * n, n)
+        out = reg.f32(out_off, n)
         rng = np.random.default_rng(22)
-        _fill(rng, a)
-        _fill(rng, b)
-        out[:] = np.nan
-        nexr.host_path_stats(reset=True)
-        nexr.reduce_copy_ptrs([reg.base + 4096 + 2048, reg.base + 4096 + 2048 + 4 * n], [reg.base + 4096 + 16], n, 7, 0,
-                              host=True)
-        st = nexr.host_path_stats()
-        assert (st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (1, 3, 0), st
-        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
-        nexr.host_deregister(ha)
-        nexr.host_path_stats(reset=True)
-        nexr.reduce_copy_ptrs([reg.base + 4096 + 2048, reg.base + 4096 + 2048 + 4 * n], [reg.base + 4096 + 16], n, 7, 0,
-                              host=True)
-        assert nexr.host_path_stats()["registeredHits"] == 3  # B's reference keeps the page
-        nexr.host_deregister(hb)
-        nexr.host_path_stats(reset=True)
-        out[:] = np.nan
-        nexr.reduce_copy_ptrs([reg.base + 4096 + 2048, reg.base + 4096 + 2048 + 4 * n], [reg.base + 4096 + 16], n, 7, 0,
-                              host=True)
-        st = nexr.host_path_stats()
-        assert (st["zeroCopyCalls"], st["registeredHits"]) == (0, 0), st
-        assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32))
+        ptrs = ([reg.base + a_off, reg.base + a_off + 4 * n], [reg.base + out_off])
+        for drop in (None, "sources", "output"):
+            _fill(rng, a)
+            _fill(rng, b)
+            out[:] = np.nan
+            nexr.host_path_stats(reset=True)
+            nexr.reduce_copy_ptrs(*ptrs, n, 7, 0, host=True)
+            st = nexr.host_path_stats()
+            assert np.array_equal(out.view(np.uint32), (a + b).view(np.uint32)), drop
+            if drop is None:
+                assert (st["zeroCopyCalls"], st["registeredHits"], st["pointerQueries"]) == (1, 3, 0), st
+                nexr.host_deregister(hs)
+            elif drop == "sources":  # out still registered and read in place; a, b found by the runtime
+                assert st["registeredHits"] == 1, st
+                nexr.host_deregister(ho)
+            else:
+                assert st["registeredHits"] == 0, st
     finally:
         reg.close()
