@@ -246,6 +246,12 @@ struct Prims {
     uint64_t head[kMaxArity];
   };
   std::deque<PendingStep> pending;
+  // Releases of queued steps not yet behind a ticket: one ticket (a hipStreamWriteValue32, ~3 us of host
+  // time) per ticketEvery steps, and always before this thread blocks (flushTicket in waitAtLeast), so
+  // a thread never waits while holding a release a peer may need.
+  PendingStep acc{0, 0, {}, {}};
+  int accSteps = 0;
+  int ticketEvery = 4;
 
   char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
   size_t slot(const Conn* q) const { return q->slotBytes ? q->slotBytes : c->stepBytes; }
@@ -298,20 +304,55 @@ struct Prims {
 
   // LL steps without a host round trip per step (round 6). Host sequencing waits for every step's
   // kernel before publishing it (streamDone), so each step costs a launch plus a wait, and the two
-  // ranks of C1 take turns: ~20 us per step. LL does not need that: its lines carry their own flags
-  // (prims_ll.h:38-93), and the kernel polls them (bounded: a flag that never comes is a timeout
-  // error, nexr_ll.hip). So a queued step publishes its send steps (incSend) as soon as its kernel is
-  // on the stream, and the receiver queues the consuming kernel at once; only the credits wait for
-  // the GPU: the slots a step read are released (postRecv, head) when its completion ticket lands
-  // (progress(), polled from every wait of this thread and by finishLL()). A kernel that polls a
-  // peer's flags must never sit in front of that peer's kernel in one hardware queue, so this is on
-  // only when the rank streams of the device fit in its hardware queues (llAsyncAllowed in
-  // nexr_ring.cpp), every rank is on one GPU (the completion word is then the step wait), and the
-  // steps run on the device.
-  void enableLLAsync() {
-    if (proto == nexrRingProtoSimple || !device || !done || !status || !c->stepWaitWord) return;
+  // ranks of C1 take turns. LL does not need that: its lines carry their own flags (prims_ll.h:38-93)
+  // and the kernel polls them (bounded: a flag that never comes is a timeout error, nexr_ll.hip). So a
+  // queued step publishes its send steps (incSend) as soon as its kernel is on the stream, the
+  // receiver queues the consuming kernel at once, and only the credits wait for the GPU: the slots a
+  // step read are released (postRecv, head) when a completion ticket behind it lands (progress(),
+  // polled from every wait of this thread and by finishLL()). A ticket is a hipStreamWriteValue32,
+  // ~3 us of host time like the launch itself (tools/api_cost_probe.cpp), so one ticket covers
+  // ticketEvery steps, and the accumulated releases are always ticketed before this thread blocks.
+  // No kernel waits behind its producer: a consumer is queued only after its producer (the tail is
+  // published after the launch returns), so on a hardware queue the two share the producer is ahead,
+  // and on separate queues both run; by induction over queueing order every polled flag arrives. The
+  // conditions (llAsyncAllowed in nexr_ring.cpp): every rank on one GPU (the completion word is the
+  // step wait), steps on the device, and the rank streams within the device's hardware queues.
+  void enableLLAsync(int every = 4) {
+    if (proto != nexrRingProtoLL || !device || !done || !status || !c->stepWaitWord) return;
     llAsync = true;
+    ticketEvery = every < 1 ? 1 : every;
     __atomic_store_n(status, 0u, __ATOMIC_RELEASE);
+  }
+  // Puts the accumulated releases behind a fresh ticket on the stream; false if the write could not be
+  // queued (the caller then drains the stream: drainLL).
+  bool flushTicket() {
+    if (acc.n == 0) return true;
+    const uint32_t t = ++done[1];
+    if (hipStreamWriteValue32(stream, done, t, 0) != hipSuccess) return false;
+    acc.ticket = t;
+    pending.push_back(acc);
+    acc.n = 0;
+    accSteps = 0;
+    return true;
+  }
+  // Every queued step complete (stream synchronised): publish every release, leave queued mode.
+  bool drainLL() {
+    llAsync = false;
+    const bool ok = hipStreamSynchronize(stream) == hipSuccess;
+    for (const PendingStep& ps : pending)
+      for (int i = 0; i < ps.n; i++) ps.conn[i]->st->head.store(ps.head[i], std::memory_order_release);
+    for (int i = 0; i < acc.n; i++) acc.conn[i]->st->head.store(acc.head[i], std::memory_order_release);
+    pending.clear();
+    acc.n = 0;
+    if (!ok) {
+      sh->fail(nexrUnhandledCudaError);
+      return false;
+    }
+    if (__atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) {
+      sh->fail(nexrInternalError);
+      return false;
+    }
+    return true;
   }
   // Publishes the heads of every queued step whose ticket has landed; false (and the communicator
   // failed) when a step's kernel reported a flag timeout.
@@ -333,6 +374,7 @@ struct Prims {
   // flowing to senders that still need credits) until the last step has completed.
   bool finishLL() {
     if (!llAsync) return true;
+    if (!flushTicket()) return drainLL();
     const uint32_t t = ++done[1];
     bool landed = false;
     if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
@@ -372,6 +414,7 @@ struct Prims {
   // abortable like checkAbort (primitives.h:142-156).
   bool waitAtLeast(std::atomic<uint64_t>& a, uint64_t target) {
     if (a.load(std::memory_order_acquire) >= target) return true;
+    if (llAsync && !flushTicket() && !drainLL()) return false;  // never block holding a release
     const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
     auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 0;; spins++) {
@@ -449,9 +492,9 @@ struct Prims {
   // LLGenericOp<RECV, SEND, SrcBuf, DstBuf> (prims_ll.h:218-283) / GenericOp of prims_ll128.h
   // (:294-331): one FIFO step per call. The sender waits for a credit (waitSend :55-75); the
   // receiver's data readiness is the line flags (NCCL_LL_FLAG(step+1), :42-43; step+1 for LL128).
-  // The host additionally waits for the sender's step so that the kernel's flag poll succeeds at
-  // once: two emulated ranks may share one GPU, and a kernel spinning on a producer that cannot be
-  // scheduled beside it must never be launched.
+  // Host-sequenced, the host additionally waits for the sender's step so that the kernel's flag poll
+  // succeeds at once; queued (enableLLAsync), the sender's tail means its kernel is on its stream, and
+  // the consuming kernel polls the flags as they arrive.
   bool genericOpLL(bool Recv, bool Send, int srcBuf, int dstBuf, int64_t srcIx, int64_t dstIx, int64_t nelem,
                    bool postOp) {
     const int nr = Recv ? nRecv : 0, ns = Send ? nSend : 0;
@@ -481,6 +524,7 @@ struct Prims {
       void* dst = dstBuf != kNone ? buf(dstBuf) + dstIx * esz : nullptr;
       const int srcIsInput = srcBuf == kInput ? 1 : 0;
       if (status && !llAsync) *status = 0;
+
       const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
       nexrResult_t r;
       if (proto == nexrRingProtoLL128)
@@ -489,24 +533,7 @@ struct Prims {
       else
         r = llFn(src, srcIsInput, nr, recvLines, rf32, dst, ns, sendLines, sf32, (size_t)nelem, datatype, devOp,
                  redOpArgs[0], postOp ? 1 : 0, status, tmo, (nexrStream_t)stream);
-      bool queued = false;
-      if (r == nexrSuccess && llAsync) {  // the ticket that releases this step's receive slots
-        const uint32_t t = ++done[1];
-        if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
-          PendingStep ps;
-          ps.ticket = t;
-          ps.n = nr;
-          for (int i = 0; i < nr; i++) {
-            ps.conn[i] = recv[i];
-            ps.head[i] = recv[i]->recvStep + 1;
-          }
-          pending.push_back(ps);
-          queued = true;
-        } else if (!finishLL()) {  // no ticket: wait for everything queued, then this step as before
-          return false;
-        }
-      }
-      if (!queued) {
+      if (!llAsync) {
         if (r == nexrSuccess && device && !streamDone()) r = nexrUnhandledCudaError;
         if (r == nexrSuccess && status && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) r = nexrInternalError;
       }
@@ -514,14 +541,20 @@ struct Prims {
         sh->fail(r);
         return false;
       }
-      if (queued) {  // postRecv waits for the ticket (progress); incSend publishes now
-        for (int i = 0; i < nr; i++) recv[i]->recvStep += 1;
-        for (int i = 0; i < ns; i++) {
-          send[i]->sendStep += 1;
-          send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
-        }
-        return progress();
+    }
+    if (llAsync) {  // queued (also an empty step, whose release must not overtake the queued ones)
+      for (int i = 0; i < nr; i++) {  // postRecv waits for a ticket (progress)
+        int j = 0;
+        while (j < acc.n && acc.conn[j] != recv[i]) j++;
+        if (j == acc.n) acc.conn[acc.n++] = recv[i];
+        acc.head[j] = ++recv[i]->recvStep;
       }
+      for (int i = 0; i < ns; i++) {  // incSend now: the receiver's kernel finds the data by its flags
+        send[i]->sendStep += 1;
+        send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
+      }
+      if (++accSteps >= ticketEvery && !flushTicket()) return drainLL();
+      return progress();
     }
     for (int i = 0; i < nr; i++) {  // postRecv (:80-83)
       recv[i]->recvStep += 1;

@@ -120,6 +120,7 @@ nexrResult_t ensurePeerLinks(nexrRingComm* c) {
       k->st = &(l->*st.state);
       if ((uncached ? hipExtMallocWithFlags((void**)&k->fifo, st.bytes, hipDeviceMallocUncached)
                     : hipMalloc((void**)&k->fifo, st.bytes)) != hipSuccess ||
+          hipMemset(k->fifo, 0, st.bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||  // no stale LL lines
           hipIpcGetMemHandle(&(l->*st.handle), k->fifo) != hipSuccess)
         return nexrUnhandledCudaError;
     }

@@ -441,7 +441,11 @@ nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes) {
   k->device = device;
   if (bytes == 0) bytes = c->cfg.buffBytes;
   if (c->cfg.memMode == nexrRingDeviceMemory) {
-    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, bytes) != hipSuccess)
+    // Zeroed, as NCCL clears its buffers: hipMalloc may hand back a freed FIFO of an earlier
+    // communicator, whose LL lines carry flags (step + 1) the new one will wait for; a queued LL
+    // consumer polls its slot before the producer writes it and must not accept such a stale line.
+    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, bytes) != hipSuccess ||
+        hipMemset(k->fifo, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
       return nexrUnhandledCudaError;
   } else if (c->needHip && pinnedHostFifos()) {
     // Host memory with the MI355X doing the steps: pinned, device-mapped FIFOs, so that a step whose
@@ -544,12 +548,17 @@ bool validConfigBuff(const nexrRingComm* c) {
          (c->proto != nexrRingProtoLL128 || c->cfg.buffBytes % (kSteps * 2048) == 0);  // whole LL128 slices
 }
 
-// Queued LL steps (Prims::enableLLAsync) for thread ranks: a kernel that polls its peer's line flags
-// must never wait behind that peer's kernel in one hardware queue, so they are on only when every rank
-// stream of the device (all channels, the tree's second streams included) can have a hardware queue of
-// its own beside the default stream's: at most GPU_MAX_HW_QUEUES - 1 of them (HIP's default is 4
-// queues per device; beyond that streams share queues). Every rank on one GPU and FIFOs in device
-// memory, as enableLLAsync requires. NEXR_LL_ASYNC=0 keeps host sequencing, =1 skips the queue count.
+// Queued LL steps (Prims::enableLLAsync) for thread ranks. LL only: an LL128 line carries one flag per
+// 128 bytes (prims_ll128.h), and a consumer polling while its producer writes could see the flag's
+// 16-B unit new and another unit of the line still old (only 16-B granules are untorn on this GPU;
+// a queued LL128 ring failed the oracle this way), while LL's flag per 8-byte granule has no such
+// window; ordering queued LL128 consumers behind producer events instead ran slower than host
+// sequencing (0.26-0.28 against 0.22 ms for C1, profiles/r06g_ll_queue_probe.json), so LL128 stays
+// host-sequenced. The kernels' progress does not depend on the hardware queues (Prims comment), but
+// as a margin the rank streams of the device (all channels, the tree's second streams included) must
+// fit in its hardware queues beside the default stream's: at most GPU_MAX_HW_QUEUES - 1 of them (HIP's
+// default is 4 per device). Every rank on one GPU and FIFOs in device memory, as enableLLAsync
+// requires. NEXR_LL_ASYNC=0 keeps host sequencing, =1 skips the queue count.
 bool llAsyncAllowed(const nexrRingComm* c) {
   static const int forced = [] {
     const char* e = getenv("NEXR_LL_ASYNC");
@@ -560,7 +569,8 @@ bool llAsyncAllowed(const nexrRingComm* c) {
     const long v = e && *e ? strtol(e, nullptr, 10) : 4;
     return v > 0 ? v : 4;
   }();
-  if (forced == 0 || !c->ll || !c->stepWaitWord || c->cfg.memMode != nexrRingDeviceMemory) return false;
+  if (forced == 0 || c->proto != nexrRingProtoLL || !c->stepWaitWord || c->cfg.memMode != nexrRingDeviceMemory)
+    return false;
   if (forced == 1) return true;
   std::vector<std::pair<int, int>> perDev;  // (device, rank streams on it)
   const int nCh = 1 + (int)c->channels.size();
@@ -576,6 +586,17 @@ bool llAsyncAllowed(const nexrRingComm* c) {
   for (const auto& d : perDev)
     if (d.second > hwQueues - 1) return false;
   return true;
+}
+
+// Queued LL steps per completion ticket (Prims::flushTicket): NEXR_LL_TICKET_EVERY, default 4 (half the
+// FIFO's 8 slots, so a sender always has credits for 4 more steps while the next ticket is pending).
+int llTicketEvery() {
+  static const int every = [] {
+    const char* e = getenv("NEXR_LL_TICKET_EVERY");
+    const long v = e && *e ? strtol(e, nullptr, 10) : 4;
+    return (int)(v < 1 ? 1 : v > 64 ? 64 : v);
+  }();
+  return every;
 }
 
 // Thread-rank collectives: the ring schedules on one thread per rank.
@@ -614,7 +635,7 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
         p.recv[p.nRecv++] = ck->conns[rank];
         p.send[p.nSend++] = ck->conns[(rank + 1) % n];
         p.attach();
-        if (llAsync) p.enableLLAsync();
+        if (llAsync) p.enableLLAsync(llTicketEvery());
         switch (coll) {
           case kAllReduce: runRingAllReduce(p, n, part); break;
           case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count, part); break;
@@ -1091,7 +1112,7 @@ NEXR_API nexrResult_t nexrPeerRingCommCreate(nexrRingComm_t* out, const nexrPeer
   const size_t allocBytes = c->cfg.buffBytes + kPeerResidentRecordBytes;
   if ((uncached ? hipExtMallocWithFlags((void**)&c->conns[me]->fifo, allocBytes, hipDeviceMallocUncached)
                 : hipMalloc((void**)&c->conns[me]->fifo, allocBytes)) != hipSuccess ||
-      hipMemset(c->conns[me]->fifo + c->cfg.buffBytes, 0, kPeerResidentRecordBytes) != hipSuccess ||
+      hipMemset(c->conns[me]->fifo, 0, allocBytes) != hipSuccess ||  // no stale LL lines (allocFifo)
       hipDeviceSynchronize() != hipSuccess)
     return fail(nexrUnhandledCudaError);
   // Rendezvous segment.

@@ -1,6 +1,7 @@
 """C1 (fp32 sum all-reduce, 4 MiB per rank, 2 thread ranks on one GPU, device memory) with the LL and
-LL128 protocols, queued steps (nexrRingCommGetLLQueued) against host-sequenced ones (NEXR_LL_ASYNC=0 in a
-child process), and the SIMPLE ring beside them; ms per call over 20 calls, every call exact. Run under
+LL128 protocols, host-sequenced (NEXR_LL_ASYNC=0) and queued (nexrRingCommGetLLQueued) with a completion
+ticket every 1, 2, 4 (default) or 7 steps (NEXR_LL_TICKET_EVERY), each in a child process, and the
+SIMPLE ring beside them; ms per call over 20 calls, every call exact. Run under
 `rocprofv3 --kernel-trace` to see the steps' kernels (tuning harness).
     python tools/ll_queue_probe.py [--child]"""
 import importlib
@@ -42,9 +43,11 @@ if __name__ == "__main__":
     if "--child" in sys.argv:
         print(json.dumps(run()))
         sys.exit(0)
-    res = {"queued": run()}
-    env = dict(os.environ, NEXR_LL_ASYNC="0")
-    p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, capture_output=True, text=True,
-                       timeout=300)
-    res["host_sequenced"] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else p.stderr[-500:]
+    res = {}
+    for tag, env in (("host_sequenced", {"NEXR_LL_ASYNC": "0"}), ("queued_ticket_every_1", {"NEXR_LL_TICKET_EVERY": "1"}),
+                     ("queued_ticket_every_2", {"NEXR_LL_TICKET_EVERY": "2"}), ("queued_ticket_every_4", {}),
+                     ("queued_ticket_every_7", {"NEXR_LL_TICKET_EVERY": "7"})):
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=300)
+        res[tag] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else p.stderr[-500:]
     print(json.dumps(res, indent=1))
