@@ -29,6 +29,7 @@ def main() -> int:
                              "allgather", "reduce", "broadcast", "sendrecv"])
     ap.add_argument("--root", type=int, default=0)
     ap.add_argument("--dt2", type=int, default=-1, help="allreduce_guard: the second call's datatype")
+    ap.add_argument("--op2", type=int, default=-1, help="allreduce_guard: the second call's op (-1: --op)")
     ap.add_argument("--shm", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -70,7 +71,7 @@ def main() -> int:
             torch.cuda.synchronize()
             t0 = time.monotonic()
             try:
-                comm.all_reduce_resident(x.data_ptr(), x.data_ptr(), a.count, a.dt2, a.op)
+                comm.all_reduce_resident(x.data_ptr(), x.data_ptr(), a.count, a.dt2, a.op if a.op2 < 0 else a.op2)
                 code = 0
             except Exception as e:  # NexrError carries the ncclResult_t value
                 code = getattr(e, "code", -1)

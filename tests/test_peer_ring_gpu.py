@@ -115,8 +115,9 @@ def test_peer_ring_resident_guard_fails_every_rank_fast(oracle, tmp_path):
     whose (datatype, op) kernel keeps fewer workgroups resident per CU must not launch a grid that
     cannot be resident beside the other ranks' grids (nexr_resident_host.cpp, the per-call capacity
     guard in residentPeerAllReduce). Nine ranks on one GPU with NEXR_RESIDENT_TEAM=128: the fp32 sum
-    kernel (58 VGPRs, 7 workgroups per CU: 1,792 on 256 CUs) agrees 128 workgroups per rank, 1,152 in
-    all; the bf16 sum kernel (99 VGPRs, 4 per CU: 1,024) cannot hold them. Every rank must return
+    kernel (60 VGPRs, 7 workgroups per CU: 1,792 on 256 CUs) agrees 128 workgroups per rank, 1,152 in
+    all; the bf16 average kernel (PreMulSum, 97 VGPRs, 4 per CU: 1,024) cannot hold them. (Until round
+    6 the bf16 sum kernel served here; the hardware-RNE fold took it to 84 VGPRs, 5 per CU: 1,280.) Every rank must return
     from the second call within seconds with InvalidUsage (its own guard) or RemoteError /
     InternalError (the shared abort word raised by another rank), and none may hang. Ranks spread over
     several GPUs share each GPU with fewer ranks, so the guard need not fire: one GPU only."""
@@ -129,7 +130,7 @@ def test_peer_ring_resident_guard_fails_every_rank_fast(oracle, tmp_path):
     from oracle.ring import ring_allreduce_expected
     n, count, buff = 9, 100_003, 1 << 18
     outs = _run_ring(tmp_path, n, mg.F32, 0, count, 0, buff, calls=1, coll="allreduce_guard",
-                     extra=("--dt2", str(mg.BF16)), env={"NEXR_RESIDENT_TEAM": "128"})
+                     extra=("--dt2", str(mg.BF16), "--op2", "4"), env={"NEXR_RESIDENT_TEAM": "128"})
     exp = ring_allreduce_expected(mg.gen_inputs(mg.F32, n, count, 7, special=True), mg.F32, 0, buff)
     codes = []
     for r in range(n):
