@@ -34,7 +34,12 @@ def instantiation(cfg) -> str:
     in the same process (C1's small ring steps, the extra configurations) never enter the median."""
     streamed = (cfg["k"] + cfg["m"]) * cfg["buf_bytes"]
     pol = 3 if streamed >= (512 << 20) else (1 if streamed >= (64 << 20) else 0)
-    return f"nexr::reduce_copy_kernel<{cfg['dt']}, {cfg['op']}, {cfg['k']}, {pol},"
+    dt = cfg["dt"]
+    # round 6 routing (nexr_api.cpp routeKernel): signed Sum / Prod / PreMulSum / SumPostDiv run the
+    # unsigned type's kernel (int8 -> uint8, int32 -> uint32, int64 -> uint64); Min / Max keep their own
+    if cfg["op"] != 2 and dt in (0, 2, 4):
+        dt += 1
+    return f"nexr::reduce_copy_kernel<{dt}, {cfg['op']}, {cfg['k']}, {pol},"
 
 
 def main():
