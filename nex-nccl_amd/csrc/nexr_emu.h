@@ -414,7 +414,16 @@ struct Prims {
   // abortable like checkAbort (primitives.h:142-156).
   bool waitAtLeast(std::atomic<uint64_t>& a, uint64_t target) {
     if (a.load(std::memory_order_acquire) >= target) return true;
-    if (llAsync && !flushTicket() && !drainLL()) return false;  // never block holding a release
+    if (llAsync && acc.n) {
+      // Never block holding a release: but a peer's post usually comes within a launch's time (~3 us),
+      // and a ticket costs as much as a launch, so look for 20 us before putting the releases behind one.
+      const auto tw = std::chrono::steady_clock::now();
+      for (unsigned spins = 1;; spins++) {
+        if (a.load(std::memory_order_acquire) >= target) return true;
+        if ((spins & 63) == 0 && std::chrono::steady_clock::now() - tw > std::chrono::microseconds(20)) break;
+      }
+      if (!flushTicket() && !drainLL()) return false;
+    }
     const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
     auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 0;; spins++) {
