@@ -129,13 +129,13 @@ NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t comm, int rank, int* up, i
  * synchronisation. NEXR_STEP_WAIT=word / sync, read once per process, forces either. */
 NEXR_API nexrResult_t nexrRingCommGetStepWait(nexrRingComm_t comm, int* word);
 
-/* Whether the last thread-rank ring collective on this communicator queued its LL steps (*queued =
- * 1): each step's kernel on the rank's stream with no host wait after it, the slots it read released
- * once a completion ticket behind it lands (one per NEXR_LL_TICKET_EVERY steps, default 4), the peer's
- * data found by the kernel's own flag poll (prims_ll.h:38-93). 0: host-sequenced (SIMPLE, LL128, ranks
- * on several GPUs, more rank streams on a GPU than it has hardware queues beside the default stream's,
- * or NEXR_LL_ASYNC=0). */
-NEXR_API nexrResult_t nexrRingCommGetLLQueued(nexrRingComm_t comm, int* queued);
+/* Whether the last thread-rank ring collective on this communicator queued its steps (*queued = 1):
+ * the LL protocol, each step's kernel on the rank's stream with no host wait after it, the peer's data
+ * found by the kernel's own flag poll (prims_ll.h:38-93), the slots a step read released once a
+ * completion ticket behind it lands (one per NEXR_LL_TICKET_EVERY steps, default 4). 0: host-sequenced
+ * (SIMPLE, LL128, ranks on several GPUs, host memory, NEXR_LL_ASYNC=0, or more rank streams on a GPU
+ * than it has hardware queues beside the default stream's). */
+NEXR_API nexrResult_t nexrRingCommGetQueued(nexrRingComm_t comm, int* queued);
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t comm);
 

@@ -973,7 +973,7 @@ NEXR_API nexrResult_t nexrRingCommGetStepWait(nexrRingComm_t c, int* word) {
   return nexrSuccess;
 }
 
-NEXR_API nexrResult_t nexrRingCommGetLLQueued(nexrRingComm_t c, int* queued) {
+NEXR_API nexrResult_t nexrRingCommGetQueued(nexrRingComm_t c, int* queued) {
   if (!c || !queued) return nexrInvalidArgument;
   *queued = c->lastLLAsync ? 1 : 0;
   return nexrSuccess;

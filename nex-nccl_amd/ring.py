@@ -20,7 +20,7 @@ RING_LIB_PATH = os.path.join(_HERE, "libnexr_ring.so")
 EXTRAS_LIB_PATH = os.path.join(_HERE, "libnexr_extras.so")
 RING_ABI_SYMBOLS = ("nexrRingCommCreate", "nexrRingAllReduce", "nexrRingReduceScatter", "nexrRingAllGather",
                     "nexrRingReduce", "nexrRingBroadcast", "nexrTreeAllReduce", "nexrTreeTopology",
-                    "nexrRingCommGetStepWait", "nexrRingCommGetLLQueued", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
+                    "nexrRingCommGetStepWait", "nexrRingCommGetQueued", "nexrRingCommDestroy", "nexrPeerRingCommCreate",
                     "nexrPeerRingAllReduce", "nexrPeerRingReduceScatter", "nexrPeerRingAllGather",
                     "nexrPeerRingReduce", "nexrPeerRingBroadcast")
 EXTRAS_ABI_SYMBOLS = ("nexrSendRecv", "nexrPeerSendRecv", "nexrRingAllReduceResident",
@@ -68,7 +68,7 @@ def _bind_ring(L: ctypes.CDLL) -> None:
         getattr(L, name).argtypes = [vp, vp, vp, sz, i32] + extra
     L.nexrTreeTopology.argtypes = [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.nexrRingCommGetStepWait.argtypes = [vp, ctypes.POINTER(i32)]
-    L.nexrRingCommGetLLQueued.argtypes = [vp, ctypes.POINTER(i32)]
+    L.nexrRingCommGetQueued.argtypes = [vp, ctypes.POINTER(i32)]
     L.nexrPeerRingCommCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(PeerRingConfig)]
     L.nexrRingCommDestroy.argtypes = [vp]
     for name in RING_ABI_SYMBOLS:
@@ -222,11 +222,11 @@ class RingComm:
         _check(self._L.nexrRingCommGetStepWait(self._h, ctypes.byref(w)), "nexrRingCommGetStepWait")
         return "word" if w.value else "sync"
 
-    def ll_queued(self) -> bool:
-        """Whether the last ring collective queued its LL / LL128 steps without a host wait per step
-        (nexrRingCommGetLLQueued)."""
+    def queued(self) -> bool:
+        """Whether the last ring collective queued its steps without a host wait per step
+        (nexrRingCommGetQueued: LL steps, every rank on one GPU, device memory)."""
         w = ctypes.c_int()
-        _check(self._L.nexrRingCommGetLLQueued(self._h, ctypes.byref(w)), "nexrRingCommGetLLQueued")
+        _check(self._L.nexrRingCommGetQueued(self._h, ctypes.byref(w)), "nexrRingCommGetQueued")
         return bool(w.value)
 
     def tree_topology(self, rank: int):

@@ -162,7 +162,7 @@ def test_ll_ring_queued_steps(ring, oracle, proto, n_ranks):
                 assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), (call, r)
             one_gpu = torch.cuda.device_count() == 1
             want = one_gpu and n_ranks <= 3 and proto == "ll"  # LL128 stays host-sequenced
-            assert comm.ll_queued() == want, (comm.ll_queued(), n_ranks, proto)
+            assert comm.queued() == want, (comm.queued(), n_ranks, proto)
 
 
 def test_ll_ring_queued_off_by_env():
@@ -185,7 +185,7 @@ recv = [torch.zeros_like(t) for t in send]
 torch.cuda.synchronize()
 with ring.RingComm(2, ring.DEVICE_MEMORY, 0, protocol=ring.PROTO_LL) as comm:
     comm.all_reduce([t.data_ptr() for t in send], [t.data_ptr() for t in recv], 300_001, 7, 0)
-    q = comm.ll_queued()
+    q = comm.queued()
 print(json.dumps({{"ok": all(np.array_equal(r.cpu().numpy(), x[0] + x[1]) for r in recv), "queued": q}}))
 """.format(root=root)
     env = dict(os.environ, NEXR_LL_ASYNC="0")
@@ -215,3 +215,50 @@ def test_ll_ring_fresh_communicators_reuse_freed_fifos(ring, oracle, proto):
                else ring_allreduce_expected_ll(inputs, dt, op, 120 * 640 * 8 * 8, proto="ll128"))
         for r in range(2):
             assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), (k, r)
+
+
+@pytest.mark.parametrize("n_ranks", [2, 3])
+def test_simple_ring_every_collective_in_a_row(ring, oracle, n_ranks):
+    """All-reduce, reduce, broadcast, reduce-scatter and all-gather in a row on one SIMPLE communicator,
+    twice, so 2-step and 1-step slices follow each other on the same FIFO slots, with a small FIFO (many
+    slot reuses per call); every rank exact against the oracle's fold order. SIMPLE steps stay
+    host-sequenced (GPU-side event ordering was no faster for C1)."""
+    from oracle.ring import (ring_allreduce_expected, reduce_scatter_expected, all_gather_expected,
+                             reduce_expected, broadcast_expected)
+    dt, op, count, buff = mg.BF16, 0, 90_001, 1 << 16
+    with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, buff, None, 20000, ring.PROTO_SIMPLE) as comm:
+        for rep in range(2):
+            inputs = mg.gen_inputs(dt, n_ranks, count, 1100 + 7 * rep + n_ranks, special=True)
+            send = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+            recv = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.all_reduce([s.data_ptr() for s in send], [d.data_ptr() for d in recv], count, dt, op)
+            assert not comm.queued()
+            exp = ring_allreduce_expected(inputs, dt, op, buff)
+            for r in range(n_ranks):
+                assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), ("ar", rep, r)
+            root = rep % n_ranks
+            rout = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.reduce([s.data_ptr() for s in send], [d.data_ptr() for d in rout], count, dt, op, root)
+            exp = reduce_expected(inputs, dt, op, root, "simple")
+            assert mg.canon_bytes(dt, rout[root].cpu().numpy()) == mg.canon_bytes(dt, exp), ("reduce", rep)
+            bout = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.broadcast([s.data_ptr() for s in send], [d.data_ptr() for d in bout], count, dt, root)
+            exp = broadcast_expected(inputs, root)
+            for r in range(n_ranks):
+                assert bout[r].cpu().numpy().tobytes() == np.asarray(exp[r]).tobytes(), ("bcast", rep, r)
+            per = count // n_ranks
+            rs = [torch.zeros(per, dtype=send[0].dtype, device="cuda") for _ in range(n_ranks)]
+            torch.cuda.synchronize()
+            comm.reduce_scatter([s.data_ptr() for s in send], [d.data_ptr() for d in rs], per, dt, op)
+            exp = reduce_scatter_expected([x[:per * n_ranks] for x in inputs], dt, op, "simple")
+            for r in range(n_ranks):
+                assert mg.canon_bytes(dt, rs[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), ("rs", rep, r)
+            ag = [torch.zeros(per * n_ranks, dtype=send[0].dtype, device="cuda") for _ in range(n_ranks)]
+            torch.cuda.synchronize()
+            comm.all_gather([s[:per].data_ptr() for s in send], [d.data_ptr() for d in ag], per, dt)
+            exp = all_gather_expected([x[:per] for x in inputs])
+            for r in range(n_ranks):
+                assert ag[r].cpu().numpy().tobytes() == exp[r].tobytes(), ("ag", rep, r)

@@ -1,5 +1,5 @@
 """C1 (fp32 sum all-reduce, 4 MiB per rank, 2 thread ranks on one GPU, device memory) with the LL and
-LL128 protocols, host-sequenced (NEXR_LL_ASYNC=0) and queued (nexrRingCommGetLLQueued) with a completion
+LL128 protocols, host-sequenced (NEXR_LL_ASYNC=0) and queued (nexrRingCommGetQueued) with a completion
 ticket every 1, 2, 4 (default) or 7 steps (NEXR_LL_TICKET_EVERY), each in a child process, and the
 SIMPLE ring beside them; ms per call over 20 calls, every call exact. Run under
 `rocprofv3 --kernel-trace` to see the steps' kernels (tuning harness).
@@ -35,7 +35,7 @@ def run():
                 comm.all_reduce([t.data_ptr() for t in send], [t.data_ptr() for t in recv], count, 7, 0)
             ms = (time.perf_counter() - t0) / 20 * 1e3
             ok = all(np.array_equal(r.cpu().numpy(), expect) for r in recv)
-            out[name] = {"ms_per_call": round(ms, 3), "exact": ok, "queued": comm.ll_queued()}
+            out[name] = {"ms_per_call": round(ms, 3), "exact": ok, "queued": comm.queued()}
     return out
 
 
