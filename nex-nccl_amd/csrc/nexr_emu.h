@@ -533,7 +533,6 @@ struct Prims {
       void* dst = dstBuf != kNone ? buf(dstBuf) + dstIx * esz : nullptr;
       const int srcIsInput = srcBuf == kInput ? 1 : 0;
       if (status && !llAsync) *status = 0;
-
       const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
       nexrResult_t r;
       if (proto == nexrRingProtoLL128)
