@@ -35,7 +35,7 @@ extern "C" {
 #define NEXR_API __attribute__((visibility("default")))
 
 #define NEXR_VERSION_MAJOR 0
-#define NEXR_VERSION_MINOR 2
+#define NEXR_VERSION_MINOR 3
 #define NEXR_VERSION_PATCH 0
 
 /* Maximum fan-in / fan-out of one call: srcs[]/dsts[] hold NCCL_MAX_ARITY+1 = 8 entries
@@ -302,6 +302,65 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
                                           const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,
                                           uint64_t redOpArg, int postOp, uint32_t* status, uint32_t timeoutUs,
                                           nexrStream_t stream);
+
+/*
+ * nexrReduceCopyLLSteps — a run of LL steps of ONE Primitives (one rank's connections of one
+ * channel) in as few launches as the steps allow, with the protocol's credits on the device: the
+ * LLGenericOp calls of a schedule (reference src/device/prims_ll.h:249-318) together with their
+ * waitSend / postRecv (:55-83), which the single-step nexrReduceCopyLL leaves to its caller.
+ *
+ * Every step of the run uses the same connections: nRecv receive FIFOs (steps with recv = 1 read all
+ * of them, as LLGenericOp<RECV=1> does) and nSend send FIFOs, each nSlots (NCCL_STEPS) slots of
+ * slotBytes. recvStep[i] / sendStep[i] are the connection's step counters at the first step of the
+ * run (the flags follow: NCCL_LL_FLAG(step + 1), :42-43); each recv / send step advances them by one.
+ * Credits live in device memory, one 8-byte word per workgroup at a 64-B stride, NEXR_LL_HEAD_BYTES
+ * per connection (zeroed when the connection is made): the receiver stores its step count into its
+ * connection's head words once it has read a step (postRecv), and a sender writes a slot only when
+ * the head words of the connection it sends into show the step NCCL_STEPS earlier read (waitSend).
+ * Both ends of a connection must therefore run their steps through this call (one workgroup of the
+ * receiver's launch frees exactly the lines one workgroup of the sender's launch writes: both derive
+ * the same grid from slotBytes). At the start of each launch the receiver stores recvStep into its
+ * head words, so a connection may switch to this call after steps run by nexrReduceCopyLL once those
+ * have completed.
+ *
+ * Element arithmetic, operand order, postOp, status and timeout as nexrReduceCopyLL, per step; user
+ * offsets in elements of `datatype` (srcBuf / dstBuf: 0 input, 1 output, -1 none). The steps run as if
+ * one at a time in order: where a step reads or writes user bytes an earlier step of the same launch
+ * wrote or read at a different element position, the library starts a new launch. A step whose line
+ * never arrives (or whose credit never comes) within timeoutUs sets *status = 1 and ends its
+ * workgroup's run; the launch never hangs. Launches are stream-ordered; the call returns after
+ * queueing them. The runs on both ends of a connection must be able to run at once: streams on
+ * hardware queues of their own (HIP shares its GPU_MAX_HW_QUEUES queues among streams and runs one
+ * queue's kernels one after the other; a stream made by hipExtStreamCreateWithCUMask has its own), and
+ * grids that fit the GPU together (one workgroup of 256 lanes per line tile of a slot, at most 64).
+ */
+#define NEXR_LL_STEPS_MAX_PEERS 3
+#define NEXR_LL_HEAD_BYTES 4096
+typedef struct {
+  int64_t srcIx, dstIx; /* element offsets into the user buffer srcBuf / dstBuf */
+  uint32_t nElts;       /* elements this step moves (0: the step only advances the counters) */
+  uint8_t recv, send;   /* RECV / SEND of LLGenericOp */
+  int8_t srcBuf, dstBuf;/* 0 input, 1 output, -1 none */
+  uint8_t postOp;
+  uint8_t pad[7];
+} nexrLLStep;           /* 32 bytes */
+typedef struct {
+  const void* input;
+  void* output;
+  int nRecv, nSend;
+  const void* recvFifo[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t* recvHead[NEXR_LL_STEPS_MAX_PEERS];       /* this rank's receive connections' head words */
+  uint64_t recvStep[NEXR_LL_STEPS_MAX_PEERS];
+  void* sendFifo[NEXR_LL_STEPS_MAX_PEERS];
+  const uint64_t* sendHead[NEXR_LL_STEPS_MAX_PEERS]; /* the receivers' head words of the send connections */
+  uint64_t sendStep[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t slotBytes; /* bytes per FIFO slot, every connection (16-B multiple) */
+  uint32_t nSlots;    /* NCCL_STEPS */
+  uint32_t pad;
+} nexrLLConnSet;
+NEXR_API nexrResult_t nexrReduceCopyLLSteps(const nexrLLConnSet* conns, const nexrLLStep* steps, int nSteps,
+                                            int datatype, int devRedOp, uint64_t redOpArg, uint32_t* status,
+                                            uint32_t timeoutUs, nexrStream_t stream);
 
 /*
  * Reduction semantics — which nex-nccl the library reproduces bit for bit. Process-wide, like an

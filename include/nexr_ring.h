@@ -129,12 +129,15 @@ NEXR_API nexrResult_t nexrTreeTopology(nexrRingComm_t comm, int rank, int* up, i
  * synchronisation. NEXR_STEP_WAIT=word / sync, read once per process, forces either. */
 NEXR_API nexrResult_t nexrRingCommGetStepWait(nexrRingComm_t comm, int* word);
 
-/* Whether the last thread-rank ring collective on this communicator queued its steps (*queued = 1):
- * the LL protocol, each step's kernel on the rank's stream with no host wait after it, the peer's data
- * found by the kernel's own flag poll (prims_ll.h:38-93), the slots a step read released once a
- * completion ticket behind it lands (one per NEXR_LL_TICKET_EVERY steps, default 4). 0: host-sequenced
- * (SIMPLE, LL128, ranks on several GPUs, host memory, NEXR_LL_ASYNC=0, or more rank streams on a GPU
- * than it has hardware queues beside the default stream's). */
+/* How the last thread-rank ring collective on this communicator ran its LL steps. *queued = 2: runs
+ * on the device (nexrReduceCopyLLSteps), up to 96 steps per launch, the peers' data found by the
+ * kernel's flag poll (prims_ll.h:38-93) and the slot credits by its poll of the receivers' head words in
+ * device memory (waitSend / postRecv, :55-83), no host wait until the collective's end (the default
+ * where 1 is possible and the communicator uses the library's own LL kernels; NEXR_LL_RUN=0 falls back
+ * to 1). 1: queued, each step's kernel on the rank's stream with no host wait after it, the slots a
+ * step read released once a completion ticket behind it lands (one per NEXR_LL_TICKET_EVERY steps,
+ * default 4). 0: host-sequenced (SIMPLE, LL128, ranks on several GPUs, host memory, NEXR_LL_ASYNC=0,
+ * or more rank streams on a GPU than it has hardware queues beside the default stream's). */
 NEXR_API nexrResult_t nexrRingCommGetQueued(nexrRingComm_t comm, int* queued);
 
 NEXR_API nexrResult_t nexrRingCommDestroy(nexrRingComm_t comm);

@@ -85,7 +85,7 @@ TYPE_SIZE = {DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Ui
 # ABI symbols declared in include/nexr.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("nexrReduceCopy", "nexrReduceCopyBatch", "nexrReduceCopyMultiDevice", "nexrReduceCopyMultiDeviceSets",
                "nexrReduceCopyHost", "nexrHostToDevRedOp", "nexrLaunchOneRank",
-               "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrQueryLaunch", "nexrGetPoolStats", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion",
+               "nexrReduceCopyLL", "nexrReduceCopyLL128", "nexrReduceCopyLLSteps", "nexrQueryLaunch", "nexrGetPoolStats", "nexrTypeSize", "nexrGetErrorString", "nexrGetVersion",
                "nexrGetLastHipError", "nexrSetSemantics", "nexrGetSemantics", "nexrHostRegister", "nexrHostDeregister",
                "nexrHostMemAlloc", "nexrHostMemFree", "nexrGetHostPathStats")
 
@@ -129,6 +129,26 @@ class ReduceCopyWork(ctypes.Structure):
     _fields_ = [("nSrcs", ctypes.c_int), ("nDsts", ctypes.c_int), ("srcs", ctypes.c_void_p * 8),
                 ("dsts", ctypes.c_void_p * 8), ("nElts", ctypes.c_size_t), ("redOpArg", ctypes.c_uint64),
                 ("nPreOpSrcs", ctypes.c_int), ("postOp", ctypes.c_int), ("preOpArgs", ctypes.c_uint64 * 8)]
+
+
+LL_STEPS_MAX_PEERS = 3  # NEXR_LL_STEPS_MAX_PEERS
+LL_HEAD_BYTES = 4096   # NEXR_LL_HEAD_BYTES
+
+
+class LLStep(ctypes.Structure):
+    """Mirror of nexrLLStep (include/nexr.h): one LLGenericOp call of a run (32 bytes)."""
+    _fields_ = [("srcIx", ctypes.c_int64), ("dstIx", ctypes.c_int64), ("nElts", ctypes.c_uint32),
+                ("recv", ctypes.c_uint8), ("send", ctypes.c_uint8), ("srcBuf", ctypes.c_int8),
+                ("dstBuf", ctypes.c_int8), ("postOp", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 7)]
+
+
+class LLConnSet(ctypes.Structure):
+    """Mirror of nexrLLConnSet (include/nexr.h): the connections a run of LL steps uses."""
+    _fields_ = [("input", ctypes.c_void_p), ("output", ctypes.c_void_p), ("nRecv", ctypes.c_int),
+                ("nSend", ctypes.c_int), ("recvFifo", ctypes.c_void_p * 3), ("recvHead", ctypes.c_void_p * 3),
+                ("recvStep", ctypes.c_uint64 * 3), ("sendFifo", ctypes.c_void_p * 3),
+                ("sendHead", ctypes.c_void_p * 3), ("sendStep", ctypes.c_uint64 * 3),
+                ("slotBytes", ctypes.c_uint64), ("nSlots", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 _lib = None
@@ -211,6 +231,8 @@ def lib() -> ctypes.CDLL:
     L.nexrReduceCopyLL128.argtypes = [vp, i32, i32, P(vp), P(u64), vp, i32, P(vp), P(u64), sz,
                                       i32, i32, u64, i32, vp, ctypes.c_uint32, vp]
     L.nexrReduceCopyLL128.restype = i32
+    L.nexrReduceCopyLLSteps.argtypes = [P(LLConnSet), P(LLStep), i32, i32, i32, u64, vp, ctypes.c_uint32, vp]
+    L.nexrReduceCopyLLSteps.restype = i32
     L.nexrTypeSize.argtypes = [i32]
     L.nexrTypeSize.restype = sz
     L.nexrGetErrorString.argtypes = [i32]
@@ -441,6 +463,38 @@ def reduce_copy_ll128(src: int, recv_wire: Sequence[int], recv_flags: Sequence[i
                                    ctypes.c_void_p(int(status)) if status else None, int(timeout_us),
                                    ctypes.c_void_p(int(stream)) if stream else None)
     _check(rc, "nexrReduceCopyLL128")
+
+
+def ll_step(src_buf: int = -1, src_ix: int = 0, dst_buf: int = -1, dst_ix: int = 0, n_elts: int = 0,
+            recv: bool = False, send: bool = False, post_op: bool = False) -> LLStep:
+    """One step of a run (buffers: 0 input, 1 output, -1 none)."""
+    s = LLStep()
+    s.srcIx, s.dstIx, s.nElts = int(src_ix), int(dst_ix), int(n_elts)
+    s.recv, s.send, s.srcBuf, s.dstBuf, s.postOp = int(bool(recv)), int(bool(send)), int(src_buf), int(dst_buf), \
+        int(bool(post_op))
+    return s
+
+
+def reduce_copy_ll_steps(input_ptr: int, output_ptr: int, recv: Sequence[tuple], send: Sequence[tuple],
+                         slot_bytes: int, steps: Sequence[LLStep], datatype: int, dev_red_op: int,
+                         red_op_arg: int = 0, n_slots: int = 8, status: int = 0, timeout_us: int = 0,
+                         stream: int = 0) -> None:
+    """A run of LL steps with device credits (nexrReduceCopyLLSteps, reference prims_ll.h:55-83 and
+    :249-318). recv / send: (fifo pointer, head-words pointer, step counter) per connection."""
+    cs = LLConnSet()
+    cs.input, cs.output = int(input_ptr) or None, int(output_ptr) or None
+    cs.nRecv, cs.nSend = len(recv), len(send)
+    for i, (fifo, head, step) in enumerate(recv):
+        cs.recvFifo[i], cs.recvHead[i], cs.recvStep[i] = int(fifo), int(head), int(step)
+    for i, (fifo, head, step) in enumerate(send):
+        cs.sendFifo[i], cs.sendHead[i], cs.sendStep[i] = int(fifo), int(head), int(step)
+    cs.slotBytes, cs.nSlots = int(slot_bytes), int(n_slots)
+    arr = (LLStep * max(1, len(steps)))(*steps)
+    rc = lib().nexrReduceCopyLLSteps(ctypes.byref(cs), arr, len(steps), int(datatype), int(dev_red_op),
+                                     int(red_op_arg) & 0xFFFFFFFFFFFFFFFF,
+                                     ctypes.c_void_p(int(status)) if status else None, int(timeout_us),
+                                     ctypes.c_void_p(int(stream)) if stream else None)
+    _check(rc, "nexrReduceCopyLLSteps")
 
 
 def version() -> int:

@@ -1449,6 +1449,121 @@ NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRec
   return nexrSuccess;
 }
 
+// The steps run as if one at a time: a launch's workgroups walk its steps independently, which is
+// only the same when no step touches user bytes that an earlier step of the launch wrote (or, for a
+// write, read) at another element position. The same range at the same position is handled by the
+// same lanes in both steps, in order.
+namespace {
+struct UserRange {
+  uintptr_t beg, end;
+  bool write;
+};
+bool rangesConflict(const std::vector<UserRange>& seen, const UserRange& r) {
+  for (const UserRange& q : seen) {
+    if (!r.write && !q.write) continue;
+    if (r.beg < q.end && q.beg < r.end && !(r.beg == q.beg && r.end == q.end)) return true;
+  }
+  return false;
+}
+}  // namespace
+
+NEXR_API nexrResult_t nexrReduceCopyLLSteps(const nexrLLConnSet* cs, const nexrLLStep* steps, int nSteps,
+                                            int datatype, int devRedOp, uint64_t redOpArg, uint32_t* status,
+                                            uint32_t timeoutUs, nexrStream_t stream) {
+  if (!cs || nSteps < 0 || (nSteps > 0 && !steps)) return nexrInvalidArgument;
+  if (cs->nRecv < 0 || cs->nRecv > NEXR_LL_STEPS_MAX_PEERS || cs->nSend < 0 || cs->nSend > NEXR_LL_STEPS_MAX_PEERS)
+    return nexrInvalidArgument;
+  if (cs->slotBytes == 0 || cs->slotBytes % 16 || cs->nSlots == 0) return nexrInvalidArgument;
+  if (datatype < 0 || datatype >= nexrNumTypes || datatype == nexrFloat8e4m3 || datatype == nexrFloat8e5m2)
+    return nexrInvalidArgument;
+  if (devRedOp < 0 || devRedOp >= nexrNumDevRedOps) return nexrInvalidArgument;
+  if (devRedOp == nexrDevSumPostDiv && !isInteger(datatype)) return nexrInvalidArgument;
+  if (devRedOp == nexrDevSumPostDiv && isSignedInt(datatype) && typeSize(datatype) == 1) {
+    uint32_t divisor = (uint32_t)(redOpArg >> 1);
+    if (divisor == 0) divisor = 1;
+    if ((int8_t)divisor == 0) return nexrInvalidArgument;
+  }
+  for (int i = 0; i < cs->nRecv; i++)
+    if (!cs->recvFifo[i] || ((uintptr_t)cs->recvFifo[i] & 15) || !cs->recvHead[i] || ((uintptr_t)cs->recvHead[i] & 7))
+      return nexrInvalidArgument;
+  for (int i = 0; i < cs->nSend; i++)
+    if (!cs->sendFifo[i] || ((uintptr_t)cs->sendFifo[i] & 15) || !cs->sendHead[i] || ((uintptr_t)cs->sendHead[i] & 7))
+      return nexrInvalidArgument;
+  const size_t esz = typeSize(datatype);
+  const uint64_t slotData = cs->slotBytes / 2;  // 8 data bytes per 16-byte line
+  for (int k = 0; k < nSteps; k++) {
+    const nexrLLStep& s = steps[k];
+    if (s.srcBuf < -1 || s.srcBuf > 1 || s.dstBuf < -1 || s.dstBuf > 1) return nexrInvalidArgument;
+    if ((s.recv && cs->nRecv == 0) || (s.send && cs->nSend == 0)) return nexrInvalidArgument;
+    if ((s.srcBuf == 0 && !cs->input) || (s.srcBuf == 1 && !cs->output) || (s.dstBuf == 0 && !cs->input) ||
+        (s.dstBuf == 1 && !cs->output))
+      return nexrInvalidArgument;
+    if (s.srcIx < 0 || s.dstIx < 0) return nexrInvalidArgument;
+    if (s.nElts == 0) continue;
+    if ((s.srcBuf < 0 && !s.recv) || (s.dstBuf < 0 && !s.send)) return nexrInvalidArgument;
+    if ((s.recv || s.send) && (uint64_t)s.nElts * esz > slotData) return nexrInvalidArgument;
+  }
+  if (nSteps == 0) return nexrSuccess;
+  int srcIsInput = 1, postOp = 1;
+  LLStepsParams P;
+  memset(&P, 0, sizeof(P));
+  llSemantics(&datatype, &devRedOp, &srcIsInput, &postOp, &P.firstWins);
+  P.input = (const char*)cs->input;
+  P.output = (char*)cs->output;
+  for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) {
+    P.recvFifo[i] = (const char*)cs->recvFifo[i];
+    P.recvHead[i] = cs->recvHead[i];
+    P.sendFifo[i] = (char*)cs->sendFifo[i];
+    P.sendHead[i] = cs->sendHead[i];
+  }
+  P.slotBytes = cs->slotBytes;
+  P.redArg = redOpArg;
+  P.status = status;
+  P.timeoutTicks = (uint64_t)(timeoutUs ? timeoutUs : 1000000u) * 100u;
+  P.nRecv = cs->nRecv;
+  P.nSend = cs->nSend;
+  P.nSlots = (int)cs->nSlots;
+  // One workgroup per line tile of a full slot (the same grid on both ends of every connection).
+  const uint64_t slotTiles = (cs->slotBytes / 16 + kLLTileLines - 1) / kLLTileLines;
+  const int grid = (int)(slotTiles < 1 ? 1 : slotTiles > (uint64_t)kLLStepsMaxGrid ? kLLStepsMaxGrid : slotTiles);
+  uint64_t rs[NEXR_LL_STEPS_MAX_PEERS], ss[NEXR_LL_STEPS_MAX_PEERS];
+  for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) rs[i] = cs->recvStep[i], ss[i] = cs->sendStep[i];
+  std::vector<UserRange> seen;
+  auto launch = [&]() -> nexrResult_t {
+    if (P.nSteps == 0) return nexrSuccess;
+    NEXR_HIP(launch_ll_steps(datatype, P, devRedOp, grid, (hipStream_t)stream));
+    P.nSteps = 0;
+    seen.clear();
+    return nexrSuccess;
+  };
+  for (int k = 0; k < nSteps; k++) {
+    const nexrLLStep& s = steps[k];
+    UserRange rd{0, 0, false}, wr{0, 0, true};
+    if (s.nElts && s.srcBuf >= 0) {
+      rd.beg = (uintptr_t)(s.srcBuf == 0 ? cs->input : cs->output) + (uintptr_t)s.srcIx * esz;
+      rd.end = rd.beg + (uintptr_t)s.nElts * esz;
+    }
+    if (s.nElts && s.dstBuf >= 0) {
+      wr.beg = (uintptr_t)(s.dstBuf == 0 ? cs->input : cs->output) + (uintptr_t)s.dstIx * esz;
+      wr.end = wr.beg + (uintptr_t)s.nElts * esz;
+    }
+    if (P.nSteps == kLLStepsMax || (rd.end && rangesConflict(seen, rd)) || (wr.end && rangesConflict(seen, wr))) {
+      nexrResult_t r = launch();
+      if (r != nexrSuccess) return r;
+    }
+    if (P.nSteps == 0)
+      for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) P.recvStep[i] = rs[i], P.sendStep[i] = ss[i];
+    P.step[P.nSteps++] = s;
+    if (rd.end) seen.push_back(rd);
+    if (wr.end) seen.push_back(wr);
+    if (s.recv)
+      for (uint64_t& v : rs) v++;
+    if (s.send)
+      for (uint64_t& v : ss) v++;
+  }
+  return launch();
+}
+
 NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int nRecv, const void* const* recvWire,
                                           const uint64_t* recvFlags, void* dst, int nSend, void* const* sendWire,
                                           const uint64_t* sendFlags, size_t nElts, int datatype, int devRedOp,

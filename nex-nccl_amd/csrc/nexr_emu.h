@@ -67,6 +67,9 @@ struct Conn {
   int device = 0;        // device of the FIFO (device memory mode)
   bool ownsFifo = true;  // false for a peer process's FIFO mapped over IPC
   bool pinned = false;   // host-memory FIFO from hipHostMalloc
+  // Thread ranks, FIFO in device memory: the receiver's head words for runs of LL steps on the device
+  // (nexrReduceCopyLLSteps), NEXR_LL_HEAD_BYTES right behind the FIFO in the same zeroed allocation.
+  uint64_t* devHead = nullptr;
   ConnState own;
   ConnState* st = &own;  // the counters: `own` for thread ranks, a shared-memory slot for process ranks
   // Each endpoint's step (the conn->step a Primitives loads and saves, prims_simple.h:528-560): only
@@ -166,7 +169,10 @@ struct nexrRingComm {
   // then land in a peer GPU's memory, and only the synchronisation is documented to cover them).
   // NEXR_STEP_WAIT=word / sync forces either (stepWaitMode).
   bool stepWaitWord = true;
-  bool lastLLAsync = false;  // whether the last thread-rank ring collective queued its LL steps (diagnostics)
+  // How the last thread-rank ring collective ran its LL steps (diagnostics, nexrRingCommGetQueued):
+  // 0 host-sequenced, 1 queued launches (Prims::enableLLAsync), 2 runs with device credits (enableLLRun).
+  int lastLLMode = 0;
+  bool ownQueues = true;  // every rank stream has a hardware queue of its own (createRankStream)
   // Frees what the extras library attached to this communicator (set by its first resident call).
   void (*freeExtras)(nexrRingComm*) = nullptr;
   // Resident ring (nexrRingAllReduceResident), made by its first call: for every device hosting ranks
@@ -252,6 +258,12 @@ struct Prims {
   PendingStep acc{0, 0, {}, {}};
   int accSteps = 0;
   int ticketEvery = 4;
+  // Runs of LL steps with the credits on the device (enableLLRun): steps collected here, launched
+  // kLLRunFlush at a time; runRecv0 / runSend0 are the connections' steps at the run's first step.
+  bool llRun = false;
+  std::vector<nexrLLStep> run;
+  uint64_t runRecv0[kMaxArity] = {}, runSend0[kMaxArity] = {};
+  static constexpr size_t kLLRunFlush = 96;  // one launch's worth (kLLStepsMax, nexr_internal.h)
 
   char* buf(int which) const { return which == kInput ? const_cast<char*>(userInput) : userOutput; }
   size_t slot(const Conn* q) const { return q->slotBytes ? q->slotBytes : c->stepBytes; }
@@ -373,6 +385,7 @@ struct Prims {
   // The end of a collective with queued steps: wait (polling, so that the heads this rank owes keep
   // flowing to senders that still need credits) until the last step has completed.
   bool finishLL() {
+    if (llRun) return finishRun();
     if (!llAsync) return true;
     if (!flushTicket()) return drainLL();
     const uint32_t t = ++done[1];
@@ -408,6 +421,73 @@ struct Prims {
       return false;
     }
     return true;
+  }
+
+  // Runs of LL steps on the device (round 6): the steps of a collective are queued as launches of up
+  // to 96 steps each (nexrReduceCopyLLSteps), whose workgroups poll the peers' line flags for the data
+  // (readLL, prims_ll.h:91-109) AND the receivers' head words for the credits (waitSend :55-75), and
+  // publish their own heads once they have read a step (postRecv :80-83) — the reference's LL loop, so
+  // the rank thread waits for nothing until the end of the collective (finishLL). The launch per step
+  // and the host hand-offs of the queued mode are gone. Conditions (llRunAllowed, nexr_ring.cpp): those
+  // of the queued mode (every rank's kernels can run at once on the one GPU), the library's own LL
+  // kernels, and device head words on every connection.
+  void enableLLRun() {
+    if (proto != nexrRingProtoLL || !device || !done || !status || !c->stepWaitWord) return;
+    if (nRecv > NEXR_LL_STEPS_MAX_PEERS || nSend > NEXR_LL_STEPS_MAX_PEERS) return;
+    for (int i = 0; i < nRecv; i++)
+      if (!recv[i]->devHead || slot(recv[i]) != c->stepBytes) return;
+    for (int i = 0; i < nSend; i++)
+      if (!send[i]->devHead || slot(send[i]) != c->stepBytes) return;
+    llRun = true;
+    run.clear();
+    __atomic_store_n(status, 0u, __ATOMIC_RELEASE);
+  }
+  bool flushRun() {
+    if (run.empty()) return true;
+    nexrLLConnSet cs;
+    memset(&cs, 0, sizeof(cs));
+    cs.input = userInput;
+    cs.output = userOutput;
+    cs.nRecv = nRecv;
+    cs.nSend = nSend;
+    for (int i = 0; i < nRecv; i++) {
+      cs.recvFifo[i] = recv[i]->fifo;
+      cs.recvHead[i] = recv[i]->devHead;
+      cs.recvStep[i] = runRecv0[i];
+    }
+    for (int i = 0; i < nSend; i++) {
+      cs.sendFifo[i] = send[i]->fifo;
+      cs.sendHead[i] = send[i]->devHead;
+      cs.sendStep[i] = runSend0[i];
+    }
+    cs.slotBytes = c->stepBytes;
+    cs.nSlots = kSteps;
+    const uint32_t tmo = (uint32_t)((c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000) * 1000u);
+    const nexrResult_t r = nexrReduceCopyLLSteps(&cs, run.data(), (int)run.size(), datatype, devOp, redOpArgs[0],
+                                                 status, tmo, (nexrStream_t)stream);
+    run.clear();
+    if (r != nexrSuccess) {
+      sh->fail(r);
+      return false;
+    }
+    return true;
+  }
+  // The end of a collective run on the device: the last launch queued, the stream complete, then the
+  // host counters (which host-sequenced collectives read) published as if every step had posted.
+  bool finishRun() {
+    llRun = false;
+    bool ok = flushRun();
+    if (!streamDone()) {
+      sh->fail(nexrUnhandledCudaError);
+      ok = false;
+    }
+    for (int i = 0; i < nRecv; i++) recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
+    for (int i = 0; i < nSend; i++) send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
+    if (ok && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) {
+      sh->fail(nexrInternalError);
+      ok = false;
+    }
+    return ok;
   }
 
   // Spin until `a` >= target (waitPeer's connStepCache loop, prims_simple.h:116-123), bounded and
@@ -508,6 +588,30 @@ struct Prims {
                    bool postOp) {
     const int nr = Recv ? nRecv : 0, ns = Send ? nSend : 0;
     nelem = nelem < 0 ? 0 : nelem;
+    if (llRun) {  // no host wait: the run's kernel polls the flags and the credits itself
+      if (sh->aborted()) {
+        sh->fail(nexrRemoteError);
+        return false;
+      }
+      if (run.empty()) {
+        for (int i = 0; i < nRecv; i++) runRecv0[i] = recv[i]->recvStep;
+        for (int i = 0; i < nSend; i++) runSend0[i] = send[i]->sendStep;
+      }
+      nexrLLStep s;
+      memset(&s, 0, sizeof(s));
+      s.srcBuf = (int8_t)(srcBuf == kNone ? -1 : srcBuf);
+      s.dstBuf = (int8_t)(dstBuf == kNone ? -1 : dstBuf);
+      s.srcIx = srcBuf == kNone ? 0 : srcIx;
+      s.dstIx = dstBuf == kNone ? 0 : dstIx;
+      s.nElts = (uint32_t)nelem;
+      s.recv = nr > 0;
+      s.send = ns > 0;
+      s.postOp = postOp ? 1 : 0;
+      run.push_back(s);
+      for (int i = 0; i < nr; i++) recv[i]->recvStep += 1;
+      for (int i = 0; i < ns; i++) send[i]->sendStep += 1;
+      return run.size() < kLLRunFlush || flushRun();
+    }
     for (int i = 0; i < ns; i++) {
       Conn* q = send[i];
       if (q->sendStep + 1 > (uint64_t)kSteps && !waitAtLeast(q->st->head, q->sendStep + 1 - kSteps)) return false;

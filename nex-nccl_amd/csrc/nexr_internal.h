@@ -50,6 +50,32 @@ struct LLParams {
 };
 hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s);
 
+// A run of LL steps of one Primitives in one launch (nexrReduceCopyLLSteps; nexr_ll.hip). Workgroup w
+// owns line tiles t = w, w + grid, ... of every step (the same lines of every slot), so the credit of a
+// slot is per workgroup: head word w of a connection holds the steps receiver workgroup w has read.
+constexpr int kLLStepsMax = 96;        // steps per launch: the parameter block stays under 4 KiB
+constexpr int kLLHeadStride = 64;      // bytes between a connection's head words
+constexpr int kLLStepsMaxGrid = NEXR_LL_HEAD_BYTES / kLLHeadStride;
+struct LLStepsParams {
+  const char* input;
+  char* output;
+  const char* recvFifo[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t* recvHead[NEXR_LL_STEPS_MAX_PEERS];
+  char* sendFifo[NEXR_LL_STEPS_MAX_PEERS];
+  const uint64_t* sendHead[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t recvStep[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t sendStep[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t slotBytes;
+  uint64_t redArg;
+  uint32_t* status;
+  uint64_t timeoutTicks;
+  int nRecv, nSend, nSlots, nSteps;
+  int firstWins;
+  nexrLLStep step[kLLStepsMax];
+};
+static_assert(sizeof(LLStepsParams) <= 4096, "kernel argument block");
+hipError_t launch_ll_steps(int dt, const LLStepsParams& a, int op, int grid, hipStream_t s);
+
 // Launch parameters of one LL128-protocol step (nexr_ll.hip; reference src/device/prims_ll128.h).
 // Wire: 2 KiB slices of 16 x 128-B lines carrying 1920 data bytes; word 15 of every line is the flag.
 constexpr int kLL128SliceBytes = 2048;

@@ -57,7 +57,8 @@ __device__ __forceinline__ void wire_st(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 
 // Slow path: poll one LL line (16 bytes at p) until both flags equal `flag`; its 8 data bytes, or
 // false after the timeout (status set).
-__device__ __forceinline__ bool poll_line(const char* p, uint32_t flag, const LLParams& a, uint64_t* data) {
+template <typename A>
+__device__ __forceinline__ bool poll_line(const char* p, uint32_t flag, const A& a, uint64_t* data) {
   uint64_t t0 = 0;
   for (;;) {
     const uint64_t w0 = ld_sys(p), w1 = ld_sys(p + 8);
@@ -121,8 +122,11 @@ __device__ __forceinline__ void st_line(char* p, uint64_t l, uint64_t nBytes, ui
 // line1}: the reduction is element-wise, so the SIMPLE path's pack arithmetic (nexr_types.hpp)
 // applies unchanged. All kLLU sub-tiles' loads of one buffer are issued before any is used.
 
-template <int D, int OP, bool IsMin>
-__device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64_t nBytes, uint64_t nLines) {
+// Returns false when one of this lane's lines never arrived (status set; its outputs unwritten).
+// A: LLParams (one step, read from the kernel arguments) or LLStepArgs (a step of a run, built in
+// registers: its peer loops are unrolled over MaxPeers so that no array is indexed at run time).
+template <int D, int OP, bool IsMin, typename A = LLParams, int MaxPeers = 1>
+__device__ __forceinline__ bool ll_tile(const A& a, uint64_t tile, uint64_t nBytes, uint64_t nLines) {
   using T = Ty<D>;
   using V = typename T::V;
   const uint64_t L0 = tile * kLLTileLines;
@@ -130,6 +134,7 @@ __device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64
   const uint32_t o0 = (threadIdx.x >> 6) * 128 + (threadIdx.x & 63);
   u32x4 d[kLLU];
   bool ok[kLLU], two[kLLU];
+  bool arrived = true;
 #pragma unroll
   for (int u = 0; u < kLLU; u++) {
     const uint32_t m0 = u * kLLSubLines + o0;
@@ -143,7 +148,8 @@ __device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64
       if (a.src && a.srcIsInput) d[u] = bc<u32x4>(T::mul(bc<V>(d[u]), T::splat(a.redArg)));  // applyPreOp
     }
   }
-  for (int i = 0; i < NEXR_MAX_SRCS; i++) {
+#pragma unroll MaxPeers
+  for (int i = 0; i < (MaxPeers > 1 ? MaxPeers : NEXR_MAX_SRCS); i++) {
     if (i >= a.nRecv) break;
     const auto r = wire_rsrc(a.recv[i] + L0 * 16, (uint64_t)tileLines * 16);
     u32x4 x0[kLLU], x1[kLLU];
@@ -164,6 +170,7 @@ __device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64
         uint64_t p0, p1 = 0;
         if (!poll_line(line, f, a, &p0) || (two[u] && !poll_line(line + 64 * 16, f, a, &p1))) {
           ok[u] = false;  // never arrived: status set, this pack's outputs stay unwritten
+          arrived = false;
           continue;
         }
         peer = (u32x4){(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
@@ -184,7 +191,8 @@ __device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64
       if (arith) d[u] = bc<u32x4>(T::canon(bc<V>(d[u])));
     }
   }
-  for (int i = 0; i < NEXR_MAX_DSTS; i++) {
+#pragma unroll MaxPeers
+  for (int i = 0; i < (MaxPeers > 1 ? MaxPeers : NEXR_MAX_DSTS); i++) {
     if (i >= a.nSend) break;
     const auto r = wire_rsrc(a.send[i] + L0 * 16, (uint64_t)tileLines * 16);
     const uint32_t f = a.sendFlag[i];
@@ -202,6 +210,7 @@ __device__ __forceinline__ void ll_tile(const LLParams& a, uint64_t tile, uint64
       if (ok[u] && two[u]) st_line(a.dst, l0 + 64, nBytes, (uint64_t)d[u].w << 32 | d[u].z);
     }
   }
+  return arrived;
 }
 
 template <int D, int OP>
@@ -248,6 +257,157 @@ hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s)
     case nexrFloat32: return launch_ll_dt<nexrFloat32>(a, op, grid, s);
     case nexrFloat64: return launch_ll_dt<nexrFloat64>(a, op, grid, s);
     case nexrBfloat16: return launch_ll_dt<nexrBfloat16>(a, op, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------------------
+// A run of LL steps in one launch (nexrReduceCopyLLSteps): LLGenericOp per step with the credit
+// protocol on the device (waitSend / postRecv, reference src/device/prims_ll.h:55-83). The reference
+// runs a step with one thread block and one head counter per connection; here a step's line tiles are
+// spread over the grid and every workgroup walks the steps on its own, so the credit is per workgroup:
+// workgroup w writes and reads the same line tiles of every slot (t = w, w + grid, ...) on both ends of a
+// connection, and head word w of the connection tells the sender's workgroup w how far the receiver's
+// workgroup w has read. No workgroup ever waits for another of its own launch.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t* head_word(uint64_t* base, uint32_t w) {
+  return base + (size_t)w * (kLLHeadStride / 8);
+}
+// waitSend's head poll (:58-62), bounded like the line polls.
+__device__ __forceinline__ bool wait_head(const uint64_t* p, uint64_t need, uint64_t timeoutTicks, uint32_t* status) {
+  uint64_t t0 = 0;
+  for (;;) {
+    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= need) return true;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (!t0) t0 = now;
+    else if (now - t0 > timeoutTicks) {
+      if (status) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+struct LLStepArgs {  // the fields of LLParams that ll_tile reads, for one step of a run
+  const char* src;
+  char* dst;
+  const char* recv[NEXR_LL_STEPS_MAX_PEERS];
+  uint32_t recvFlag[NEXR_LL_STEPS_MAX_PEERS];
+  char* send[NEXR_LL_STEPS_MAX_PEERS];
+  uint32_t sendFlag[NEXR_LL_STEPS_MAX_PEERS];
+  uint64_t redArg;
+  uint32_t* status;
+  uint64_t timeoutTicks;
+  int nRecv, nSend, srcIsInput, postOp, firstWins;
+};
+
+template <int D, int OP>
+__global__ __launch_bounds__(kBlock) void reduce_copy_ll_steps_kernel(LLStepsParams P) {
+  constexpr uint64_t esz = 16 / Ty<D>::EPP;
+  __shared__ int sNoCredit;
+  const uint32_t w = blockIdx.x, G = gridDim.x;
+  uint64_t rs[NEXR_LL_STEPS_MAX_PEERS], ss[NEXR_LL_STEPS_MAX_PEERS];
+#pragma unroll
+  for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) rs[i] = P.recvStep[i], ss[i] = P.sendStep[i];
+  // Every earlier step of this stream has completed: whatever ran them, the slots before recvStep are read.
+  if (threadIdx.x == 0) {
+    sNoCredit = 0;
+    for (int i = 0; i < P.nRecv; i++)
+      __hip_atomic_store(head_word(P.recvHead[i], w), rs[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  constexpr int MP = NEXR_LL_STEPS_MAX_PEERS;
+  LLStepArgs a;
+  a.redArg = P.redArg;
+  a.status = P.status;
+  a.timeoutTicks = P.timeoutTicks;
+  a.firstWins = P.firstWins;
+  for (int k = 0; k < P.nSteps; k++) {
+    const nexrLLStep& st = P.step[k];
+    const uint64_t nBytes = (uint64_t)st.nElts * esz;
+    const uint64_t nLines = (nBytes + 7) / 8;
+    const uint64_t nTiles = (nLines + kLLTileLines - 1) / kLLTileLines;
+    if (w < nTiles) {
+      if (st.send) {  // waitSend: the receiver's workgroup w has read the step nSlots back
+        if (threadIdx.x == 0) {
+          for (int j = 0; j < P.nSend; j++)
+            if (ss[j] + 1 > (uint64_t)P.nSlots &&
+                !wait_head(head_word(const_cast<uint64_t*>(P.sendHead[j]), w), ss[j] + 1 - P.nSlots,
+                           P.timeoutTicks, P.status))
+              sNoCredit = 1;
+        }
+        __syncthreads();
+        if (sNoCredit) return;
+      }
+      a.src = st.srcBuf == 0 ? P.input + st.srcIx * esz : st.srcBuf == 1 ? P.output + st.srcIx * esz : nullptr;
+      a.dst = st.dstBuf == 0 ? const_cast<char*>(P.input) + st.dstIx * esz
+              : st.dstBuf == 1 ? P.output + st.dstIx * esz : nullptr;
+      a.nRecv = st.recv ? P.nRecv : 0;
+      a.nSend = st.send ? P.nSend : 0;
+#pragma unroll
+      for (int i = 0; i < MP; i++) {
+        a.recv[i] = P.recvFifo[i] + (rs[i] % P.nSlots) * P.slotBytes;
+        a.recvFlag[i] = (uint32_t)(rs[i] + 1);
+        a.send[i] = P.sendFifo[i] + (ss[i] % P.nSlots) * P.slotBytes;
+        a.sendFlag[i] = (uint32_t)(ss[i] + 1);
+      }
+      a.srcIsInput = st.srcBuf == 0 && !P.firstWins;
+      a.postOp = st.postOp && !P.firstWins;
+      bool arrived = true;
+      for (uint64_t t = w; t < nTiles; t += G) {
+        if constexpr (OP == nexrDevMinMax) {
+          if ((a.redArg & 1) == 0) arrived &= ll_tile<D, OP, true, LLStepArgs, MP>(a, t, nBytes, nLines);
+          else arrived &= ll_tile<D, OP, false, LLStepArgs, MP>(a, t, nBytes, nLines);
+        } else {
+          arrived &= ll_tile<D, OP, false, LLStepArgs, MP>(a, t, nBytes, nLines);
+        }
+      }
+      if (__syncthreads_or(!arrived)) return;  // a line never came: status set, this workgroup stops
+    }
+    if (st.recv) {  // postRecv: every lane's reads of the step are done (barrier), then the head
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int i = 0; i < P.nRecv; i++)
+          __hip_atomic_store(head_word(P.recvHead[i], w), rs[i] + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) rs[i]++;
+    }
+    if (st.send) {
+#pragma unroll
+      for (int j = 0; j < NEXR_LL_STEPS_MAX_PEERS; j++) ss[j]++;
+    }
+  }
+}
+
+template <int D>
+static hipError_t launch_ll_steps_dt(const LLStepsParams& a, int op, int grid, hipStream_t s) {
+  const void* fn = nullptr;
+  switch (op) {
+    case nexrDevSum: fn = (const void*)&reduce_copy_ll_steps_kernel<D, nexrDevSum>; break;
+    case nexrDevProd: fn = (const void*)&reduce_copy_ll_steps_kernel<D, nexrDevProd>; break;
+    case nexrDevMinMax: fn = (const void*)&reduce_copy_ll_steps_kernel<D, nexrDevMinMax>; break;
+    case nexrDevPreMulSum: fn = (const void*)&reduce_copy_ll_steps_kernel<D, nexrDevPreMulSum>; break;
+    case nexrDevSumPostDiv:
+      if constexpr (Ty<D>::kIsInt) fn = (const void*)&reduce_copy_ll_steps_kernel<D, nexrDevSumPostDiv>;
+      break;
+  }
+  if (!fn) return hipErrorInvalidValue;
+  void* args[] = {const_cast<LLStepsParams*>(&a)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, 0, s);
+}
+
+hipError_t launch_ll_steps(int dt, const LLStepsParams& a, int op, int grid, hipStream_t s) {
+  switch (dt) {
+    case nexrInt8: return launch_ll_steps_dt<nexrInt8>(a, op, grid, s);
+    case nexrUint8: return launch_ll_steps_dt<nexrUint8>(a, op, grid, s);
+    case nexrInt32: return launch_ll_steps_dt<nexrInt32>(a, op, grid, s);
+    case nexrUint32: return launch_ll_steps_dt<nexrUint32>(a, op, grid, s);
+    case nexrInt64: return launch_ll_steps_dt<nexrInt64>(a, op, grid, s);
+    case nexrUint64: return launch_ll_steps_dt<nexrUint64>(a, op, grid, s);
+    case nexrFloat16: return launch_ll_steps_dt<nexrFloat16>(a, op, grid, s);
+    case nexrFloat32: return launch_ll_steps_dt<nexrFloat32>(a, op, grid, s);
+    case nexrFloat64: return launch_ll_steps_dt<nexrFloat64>(a, op, grid, s);
+    case nexrBfloat16: return launch_ll_steps_dt<nexrBfloat16>(a, op, grid, s);
   }
   return hipErrorInvalidValue;
 }

@@ -327,6 +327,33 @@ nexrResult_t allocDone(uint32_t** w) {
   return nexrSuccess;
 }
 
+// A rank stream. Runs of LL steps on the device (Prims::enableLLRun) need the ranks' kernels to run at
+// the same time: HIP shares its GPU_MAX_HW_QUEUES hardware queues among streams (once they are all made,
+// a new stream takes the least used one), and two streams on one queue run their kernels one after the
+// other, so a run waiting for its peer's would end only at its timeout. A stream made with a CU mask gets a
+// hardware queue of its own (the runtime does not share those); with every CU in the mask it runs like any
+// other stream (tools/ll_run_queue_probe.py). Device-memory communicators make their rank streams so
+// (NEXR_RING_OWN_QUEUES=0: plain streams, and no device runs); *own reports whether it worked.
+hipError_t createRankStream(const nexrRingComm* c, hipStream_t* s, bool* own) {
+  static const bool off = [] {
+    const char* e = getenv("NEXR_RING_OWN_QUEUES");
+    return e && e[0] == '0';
+  }();
+  *own = false;
+  int dev = 0, cus = 0;
+  if (c->cfg.memMode == nexrRingDeviceMemory && !off && hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+    if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+      *own = true;
+      return hipSuccess;
+    }
+    (void)hipGetLastError();
+  }
+  return hipStreamCreate(s);
+}
+
 // The completion word of `stream` (one of the communicator's streams), or nullptr.
 uint32_t* doneFor(const nexrRingComm* c, hipStream_t stream) {
   if (!stream) return nullptr;
@@ -444,9 +471,11 @@ nexrResult_t allocFifo(nexrRingComm* c, Conn* k, int device, size_t bytes) {
     // Zeroed, as NCCL clears its buffers: hipMalloc may hand back a freed FIFO of an earlier
     // communicator, whose LL lines carry flags (step + 1) the new one will wait for; a queued LL
     // consumer polls its slot before the producer writes it and must not accept such a stale line.
-    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, bytes) != hipSuccess ||
-        hipMemset(k->fifo, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    // The receiver's head words for runs of LL steps (Conn::devHead) follow the FIFO, zeroed with it.
+    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&k->fifo, bytes + NEXR_LL_HEAD_BYTES) != hipSuccess ||
+        hipMemset(k->fifo, 0, bytes + NEXR_LL_HEAD_BYTES) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
       return nexrUnhandledCudaError;
+    k->devHead = (uint64_t*)(k->fifo + bytes);
   } else if (c->needHip && pinnedHostFifos()) {
     // Host memory with the MI355X doing the steps: pinned, device-mapped FIFOs, so that a step whose
     // user buffers are pinned too runs as one zero-copy kernel over PCIe (nexrReduceCopyHost) instead
@@ -492,8 +521,10 @@ nexrResult_t ensureSecondStreams(nexrRingComm* c) {
   c->done2.assign(n, nullptr);
   for (int r = 0; r < n; r++) {
     if (c->streams[r]) {
-      if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams2[r]) != hipSuccess)
+      bool own = false;
+      if (hipSetDevice(c->devices[r]) != hipSuccess || createRankStream(c, &c->streams2[r], &own) != hipSuccess)
         return nexrUnhandledCudaError;
+      c->ownQueues = c->ownQueues && own;
       if (allocDone(&c->done2[r]) != nexrSuccess) return nexrUnhandledCudaError;
     }
     if (c->ll) {
@@ -588,6 +619,20 @@ bool llAsyncAllowed(const nexrRingComm* c) {
   return true;
 }
 
+// Runs of LL steps on the device (Prims::enableLLRun): where the queued mode may run (every rank's
+// kernels can run at once on the one GPU), with the library's own LL kernels (not a caller's llFn).
+// NEXR_LL_RUN=0 falls back to queued launches.
+bool llRunAllowed(const nexrRingComm* c, bool llAsync) {
+  static const bool off = [] {
+    const char* e = getenv("NEXR_LL_RUN");
+    return e && e[0] == '0';
+  }();
+  if (!llAsync || off || c->cfg.llFn != defaultLLFn || !c->ownQueues) return false;
+  for (const nexrRingComm* ck : c->channels)
+    if (!ck->ownQueues) return false;
+  return true;
+}
+
 // Queued LL steps per completion ticket (Prims::flushTicket): NEXR_LL_TICKET_EVERY, default 4 (half the
 // FIFO's 8 slots, so a sender always has credits for 4 more steps while the next ticket is pending).
 int llTicketEvery() {
@@ -623,7 +668,8 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
   for (ChannelPart& part : parts) part.chunkCount = chunkElems(channelComm(c, part.channel), g, esz, false, 0);
   Shared sh;
   const bool llAsync = llAsyncAllowed(c);
-  c->lastLLAsync = llAsync;
+  const bool llRun = llRunAllowed(c, llAsync);
+  c->lastLLMode = llRun ? 2 : llAsync ? 1 : 0;
   std::vector<std::function<void()>> jobs;
   for (const ChannelPart& part : parts) {
     for (int rank = 0; rank < n; rank++) {
@@ -635,7 +681,8 @@ nexrResult_t ringCollective(nexrRingComm* c, RingColl coll, const void* const* s
         p.recv[p.nRecv++] = ck->conns[rank];
         p.send[p.nSend++] = ck->conns[(rank + 1) % n];
         p.attach();
-        if (llAsync) p.enableLLAsync(llTicketEvery());
+        if (llRun) p.enableLLRun();
+        if (llAsync && !p.llRun) p.enableLLAsync(llTicketEvery());
         switch (coll) {
           case kAllReduce: runRingAllReduce(p, n, part); break;
           case kReduceScatter: runRingReduceScatter(p, n, (int64_t)count, part); break;
@@ -824,11 +871,13 @@ NEXR_API nexrResult_t nexrRingCommCreate(nexrRingComm_t* out, const nexrRingConf
   for (int r = 0; r < n; r++) {
     c->conns.push_back(new Conn());
     if (nDev > 0) {
-      if (hipSetDevice(c->devices[r]) != hipSuccess || hipStreamCreate(&c->streams[r]) != hipSuccess ||
+      bool own = false;
+      if (hipSetDevice(c->devices[r]) != hipSuccess || createRankStream(c, &c->streams[r], &own) != hipSuccess ||
           allocDone(&c->done[r]) != nexrSuccess) {
         nexrRingCommDestroy(c);
         return nexrUnhandledCudaError;
       }
+      c->ownQueues = c->ownQueues && own;
     }
     nexrResult_t res = c->ll ? allocStatus(c, &c->status[r]) : nexrSuccess;
     if (res == nexrSuccess) res = allocFifo(c, c->conns[r], c->devices[r]);
@@ -975,7 +1024,7 @@ NEXR_API nexrResult_t nexrRingCommGetStepWait(nexrRingComm_t c, int* word) {
 
 NEXR_API nexrResult_t nexrRingCommGetQueued(nexrRingComm_t c, int* queued) {
   if (!c || !queued) return nexrInvalidArgument;
-  *queued = c->lastLLAsync ? 1 : 0;
+  *queued = c->lastLLMode;
   return nexrSuccess;
 }
 

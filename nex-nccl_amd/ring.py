@@ -222,12 +222,13 @@ class RingComm:
         _check(self._L.nexrRingCommGetStepWait(self._h, ctypes.byref(w)), "nexrRingCommGetStepWait")
         return "word" if w.value else "sync"
 
-    def queued(self) -> bool:
-        """Whether the last ring collective queued its steps without a host wait per step
-        (nexrRingCommGetQueued: LL steps, every rank on one GPU, device memory)."""
+    def queued(self) -> int:
+        """How the last ring collective ran its LL steps (nexrRingCommGetQueued): 2 runs on the device
+        with device credits, 1 queued launches, 0 host-sequenced (LL steps need every rank on one GPU
+        and device memory for 1 or 2)."""
         w = ctypes.c_int()
         _check(self._L.nexrRingCommGetQueued(self._h, ctypes.byref(w)), "nexrRingCommGetQueued")
-        return bool(w.value)
+        return int(w.value)
 
     def tree_topology(self, rank: int):
         """(up, [down...]) of `rank` in this communicator's tree (-1 = none)."""

@@ -59,7 +59,7 @@ def test_type_size_and_strings(nexr):
         assert L.nexrTypeSize(int(dt)) == sz
     assert L.nexrTypeSize(12) == 0
     assert L.nexrGetErrorString(4) == b"invalid argument"
-    assert nexr.version() == 200
+    assert nexr.version() == 300
 
 
 def _call(nexr, nsrcs=2, ndsts=1, n=16, dt=7, op=0, arg=0, pre=None, srcs=None, dsts=None):
@@ -301,6 +301,89 @@ def test_batch_work_layout_matches_header(nexr):
     assert (W.srcs.offset, W.dsts.offset, W.nElts.offset, W.preOpArgs.offset) == (8, 72, 136, 160)
     assert re.search(r"#define\s+NEXR_MAX_BATCH_WORKS\s+(\d+)", open(HEADER).read()).group(1) == str(
         nexr.MAX_BATCH_WORKS)
+
+
+_LL_STEPS_LAYOUT = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include "nexr.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(nexrLLStep), offsetof(nexrLLStep, srcIx),
+         offsetof(nexrLLStep, dstIx), offsetof(nexrLLStep, nElts), offsetof(nexrLLStep, recv),
+         offsetof(nexrLLStep, send), offsetof(nexrLLStep, srcBuf), offsetof(nexrLLStep, dstBuf),
+         offsetof(nexrLLStep, postOp));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(nexrLLConnSet), offsetof(nexrLLConnSet, nRecv),
+         offsetof(nexrLLConnSet, recvFifo), offsetof(nexrLLConnSet, recvHead), offsetof(nexrLLConnSet, recvStep),
+         offsetof(nexrLLConnSet, sendFifo), offsetof(nexrLLConnSet, sendHead), offsetof(nexrLLConnSet, sendStep),
+         offsetof(nexrLLConnSet, slotBytes), offsetof(nexrLLConnSet, nSlots), offsetof(nexrLLConnSet, pad));
+  return 0;
+}
+"""
+
+
+def test_ll_steps_structs_match_header(nexr, tmp_path):
+    """nexrLLStep / nexrLLConnSet (ABI 0.3): the C layout (compiled from include/nexr.h) and the ctypes
+    mirror agree field by field; a step is 32 bytes (kLLStepsMax of them fit one launch's 4 KiB)."""
+    src = tmp_path / "ll_steps_layout.c"
+    src.write_text(_LL_STEPS_LAYOUT)
+    exe = tmp_path / "ll_steps_layout"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe)], check=True, capture_output=True, text=True, timeout=120)
+    step, conns = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines()
+    S, C = nexr.LLStep, nexr.LLConnSet
+    assert step.split() == [str(v) for v in (ctypes.sizeof(S), S.srcIx.offset, S.dstIx.offset, S.nElts.offset,
+                                               S.recv.offset, S.send.offset, S.srcBuf.offset, S.dstBuf.offset,
+                                               S.postOp.offset)]
+    assert ctypes.sizeof(S) == 32
+    assert conns.split() == [str(v) for v in (ctypes.sizeof(C), C.nRecv.offset, C.recvFifo.offset, C.recvHead.offset,
+                                                C.recvStep.offset, C.sendFifo.offset, C.sendHead.offset,
+                                                C.sendStep.offset, C.slotBytes.offset, C.nSlots.offset,
+                                                C.pad.offset)]
+    hdr = open(HEADER).read()
+    assert re.search(r"#define\s+NEXR_LL_STEPS_MAX_PEERS\s+(\d+)", hdr).group(1) == str(nexr.LL_STEPS_MAX_PEERS)
+    assert re.search(r"#define\s+NEXR_LL_HEAD_BYTES\s+(\d+)", hdr).group(1) == str(nexr.LL_HEAD_BYTES)
+
+
+def test_ll_steps_validate_before_the_device(nexr):
+    """nexrReduceCopyLLSteps rejects a bad connection set or step before anything is launched."""
+    L = nexr.lib()
+    fifo, head, slot = 0x100000, 0x200000, 1 << 16
+
+    def call(conns, steps, dt=7, op=0):
+        arr = (nexr.LLStep * max(1, len(steps)))(*steps)
+        return L.nexrReduceCopyLLSteps(ctypes.byref(conns) if conns is not None else None, arr, len(steps), dt, op,
+                                       0, None, 0, None)
+
+    def conns(n_recv=1, n_send=1, slot_bytes=slot, n_slots=8, inp=0x10000, out=0x20000):
+        c = nexr.LLConnSet()
+        c.input, c.output, c.nRecv, c.nSend = inp, out, n_recv, n_send
+        for i in range(min(n_recv, 3)):
+            c.recvFifo[i], c.recvHead[i] = fifo, head
+        for i in range(min(n_send, 3)):
+            c.sendFifo[i], c.sendHead[i] = fifo + slot * 8, head + 4096
+        c.slotBytes, c.nSlots = slot_bytes, n_slots
+        return c
+
+    ok = nexr.ll_step(0, 0, 1, 0, 100, recv=True, send=True)
+    assert call(conns(), []) == 0                                    # nothing to run
+    assert call(None, [ok]) == 4
+    assert call(conns(n_recv=4), [ok]) == 4                          # > NEXR_LL_STEPS_MAX_PEERS
+    assert call(conns(slot_bytes=1000), [ok]) == 4                   # not a 16-B multiple
+    assert call(conns(n_slots=0), [ok]) == 4
+    assert call(conns(), [ok], dt=10) == 4                           # fp8
+    assert call(conns(), [ok], dt=7, op=4) == 4                      # SumPostDiv on a float
+    bad_fifo = conns()
+    bad_fifo.recvFifo[0] = fifo + 8                                  # FIFO not 16-B aligned
+    assert call(bad_fifo, [ok]) == 4
+    bad_head = conns()
+    bad_head.sendHead[0] = 0
+    assert call(bad_head, [ok]) == 4
+    assert call(conns(n_recv=0), [ok]) == 4                          # a recv step without receive connections
+    assert call(conns(), [nexr.ll_step(0, 0, 1, 0, slot // 2 // 4 + 1, recv=True)]) == 4  # more than a slot's data
+    assert call(conns(), [nexr.ll_step(-1, 0, 1, 0, 100)]) == 4      # no source and no receive
+    assert call(conns(), [nexr.ll_step(0, 0, 2, 0, 100)]) == 4       # dstBuf out of range
+    assert call(conns(out=0), [nexr.ll_step(0, 0, 1, 0, 100)]) == 4  # output buffer missing
+    assert call(conns(), [ok, nexr.ll_step(0, -1, 1, 0, 100)]) == 4  # a later bad step: nothing runs
 
 
 def test_batch_validates_every_work_before_launching(nexr):

@@ -139,12 +139,12 @@ def test_step_wait_modes_give_the_same_results(wait):
 @pytest.mark.parametrize("proto", ["ll", "ll128"])
 @pytest.mark.parametrize("n_ranks", [2, 3, 4])
 def test_ll_ring_queued_steps(ring, oracle, proto, n_ranks):
-    """Round 6: LL ring steps queued on each rank's stream with no host wait per step (the kernel finds
-    the peer's data by its line flags; a step's receive slots are released when a completion ticket
-    behind it lands). On one GPU they queue while the rank streams fit beside the default stream in
-    HIP's 4 hardware queues (2 and 3 ranks); 4 ranks and LL128 (one flag per 128-B line) stay
-    host-sequenced. Three calls in a row on one communicator (the step counters and flags carry over),
-    every rank exact against the oracle's LL fold order."""
+    """Round 6: LL ring steps without a host wait per step. On one GPU, while the rank streams fit beside
+    the default stream in HIP's 4 hardware queues (2 and 3 ranks), they run on the device
+    (nexrReduceCopyLLSteps: up to 96 steps per launch, the peer's data found by its line flags and the
+    slot credits by the receivers' head words; nexrRingCommGetQueued = 2); 4 ranks and LL128 (one flag
+    per 128-B line) stay host-sequenced (0). Three calls in a row on one communicator (the step
+    counters, flags and head words carry over), every rank exact against the oracle's LL fold order."""
     from oracle.ring import ring_allreduce_expected_ll
     dt, op = (mg.F32, 0) if proto == "ll" else (mg.BF16, 0)
     count = 600_007
@@ -161,13 +161,14 @@ def test_ll_ring_queued_steps(ring, oracle, proto, n_ranks):
             for r in range(n_ranks):
                 assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), (call, r)
             one_gpu = torch.cuda.device_count() == 1
-            want = one_gpu and n_ranks <= 3 and proto == "ll"  # LL128 stays host-sequenced
+            want = 2 if one_gpu and n_ranks <= 3 and proto == "ll" else 0  # LL128 stays host-sequenced
             assert comm.queued() == want, (comm.queued(), n_ranks, proto)
 
 
-def test_ll_ring_queued_off_by_env():
-    """NEXR_LL_ASYNC=0 (read once per process) keeps host-sequenced LL steps: same exact sums, and the
-    communicator reports that it did not queue."""
+@pytest.mark.parametrize("env,want", [({"NEXR_LL_ASYNC": "0"}, 0), ({"NEXR_LL_RUN": "0"}, 1)])
+def test_ll_ring_modes_by_env(env, want):
+    """NEXR_LL_ASYNC=0 (read once per process) keeps host-sequenced LL steps, NEXR_LL_RUN=0 the queued
+    launches of one step each: same exact sums, and the communicator reports the mode it ran."""
     import json
     import os
     import subprocess
@@ -188,11 +189,12 @@ with ring.RingComm(2, ring.DEVICE_MEMORY, 0, protocol=ring.PROTO_LL) as comm:
     q = comm.queued()
 print(json.dumps({{"ok": all(np.array_equal(r.cpu().numpy(), x[0] + x[1]) for r in recv), "queued": q}}))
 """.format(root=root)
-    env = dict(os.environ, NEXR_LL_ASYNC="0")
-    out = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, timeout=150)
+    out = subprocess.run([sys.executable, "-c", script], env=dict(os.environ, **env), capture_output=True, text=True,
+                         timeout=150)
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
-    assert d == {"ok": True, "queued": False}, d
+    one_gpu = torch.cuda.device_count() == 1
+    assert d == {"ok": True, "queued": want if one_gpu else 0}, d
 
 
 @pytest.mark.parametrize("proto", ["ll", "ll128"])
@@ -254,6 +256,60 @@ def test_simple_ring_every_collective_in_a_row(ring, oracle, n_ranks):
             torch.cuda.synchronize()
             comm.reduce_scatter([s.data_ptr() for s in send], [d.data_ptr() for d in rs], per, dt, op)
             exp = reduce_scatter_expected([x[:per * n_ranks] for x in inputs], dt, op, "simple")
+            for r in range(n_ranks):
+                assert mg.canon_bytes(dt, rs[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), ("rs", rep, r)
+            ag = [torch.zeros(per * n_ranks, dtype=send[0].dtype, device="cuda") for _ in range(n_ranks)]
+            torch.cuda.synchronize()
+            comm.all_gather([s[:per].data_ptr() for s in send], [d.data_ptr() for d in ag], per, dt)
+            exp = all_gather_expected([x[:per] for x in inputs])
+            for r in range(n_ranks):
+                assert ag[r].cpu().numpy().tobytes() == exp[r].tobytes(), ("ag", rep, r)
+
+
+@pytest.mark.parametrize("n_ranks,buff", [(2, 1 << 16), (3, 1 << 16), (2, 0)])
+def test_ll_runs_every_collective_in_a_row(ring, oracle, n_ranks, buff):
+    """Every ring collective with the LL protocol on one communicator, twice, as device runs
+    (nexrReduceCopyLLSteps): all-reduce out of place and in place, reduce, broadcast,
+    reduce-scatter and all-gather, a 64 KiB FIFO (8 KiB slots: one workgroup, hundreds of slot reuses per
+    call) and the default 512 KiB (eight workgroups), bf16 average (the pre-op on every input); every
+    rank exact against the oracle's LL fold order (peer first)."""
+    from oracle.ring import (ring_allreduce_expected_ll, reduce_scatter_expected, all_gather_expected,
+                             reduce_expected, broadcast_expected)
+    dt, op, count = mg.BF16, 4, 150_001
+    with ring.RingComm(n_ranks, ring.DEVICE_MEMORY, buff, None, 20000, ring.PROTO_LL) as comm:
+        for rep in range(2):
+            inputs = mg.gen_inputs(dt, n_ranks, count, 1300 + 7 * rep + n_ranks, special=True)
+            send = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+            recv = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.all_reduce([s.data_ptr() for s in send], [d.data_ptr() for d in recv], count, dt, op)
+            if torch.cuda.device_count() == 1:
+                assert comm.queued() == 2
+            exp = ring_allreduce_expected_ll(inputs, dt, op, buff or 8 * 512 * 8 * 16)
+            for r in range(n_ranks):
+                assert mg.canon_bytes(dt, recv[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), ("ar", rep, r)
+            inplace = [torch.from_numpy(x.copy()).cuda() for x in inputs]
+            torch.cuda.synchronize()
+            comm.all_reduce([s.data_ptr() for s in inplace], [s.data_ptr() for s in inplace], count, dt, op)
+            for r in range(n_ranks):
+                assert mg.canon_bytes(dt, inplace[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), ("in place", rep, r)
+            root = (rep + 1) % n_ranks
+            rout = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.reduce([s.data_ptr() for s in send], [d.data_ptr() for d in rout], count, dt, op, root)
+            exp = reduce_expected(inputs, dt, op, root, "ll")
+            assert mg.canon_bytes(dt, rout[root].cpu().numpy()) == mg.canon_bytes(dt, exp), ("reduce", rep)
+            bout = [torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+            comm.broadcast([s.data_ptr() for s in send], [d.data_ptr() for d in bout], count, dt, root)
+            exp = broadcast_expected(inputs, root)
+            for r in range(n_ranks):
+                assert bout[r].cpu().numpy().tobytes() == np.asarray(exp[r]).tobytes(), ("bcast", rep, r)
+            per = count // n_ranks
+            rs = [torch.zeros(per, dtype=send[0].dtype, device="cuda") for _ in range(n_ranks)]
+            torch.cuda.synchronize()
+            comm.reduce_scatter([s.data_ptr() for s in send], [d.data_ptr() for d in rs], per, dt, op)
+            exp = reduce_scatter_expected([x[:per * n_ranks] for x in inputs], dt, op, "ll")
             for r in range(n_ranks):
                 assert mg.canon_bytes(dt, rs[r].cpu().numpy()) == mg.canon_bytes(dt, exp[r]), ("rs", rep, r)
             ag = [torch.zeros(per * n_ranks, dtype=send[0].dtype, device="cuda") for _ in range(n_ranks)]

@@ -1,7 +1,8 @@
 """C1 (fp32 sum all-reduce, 4 MiB per rank, 2 thread ranks on one GPU, device memory) with the LL and
-LL128 protocols, host-sequenced (NEXR_LL_ASYNC=0) and queued (nexrRingCommGetQueued) with a completion
-ticket every 1, 2, 4 (default) or 7 steps (NEXR_LL_TICKET_EVERY), each in a child process, and the
-SIMPLE ring beside them; ms per call over 20 calls, every call exact. Run under
+LL128 protocols, host-sequenced (NEXR_LL_ASYNC=0), queued launches with a completion ticket every 4
+steps (NEXR_LL_RUN=0) and device runs (the default; nexrRingCommGetQueued reports which), each in a
+child process, and the SIMPLE ring beside them (round 6 also measured tickets every 1, 2 and 7 steps
+with NEXR_LL_TICKET_EVERY, profiles/r06e_*, r06g_*); ms per call over 20 calls, every call exact. Run under
 `rocprofv3 --kernel-trace` to see the steps' kernels (tuning harness).
     python tools/ll_queue_probe.py [--child]"""
 import importlib
@@ -44,9 +45,8 @@ if __name__ == "__main__":
         print(json.dumps(run()))
         sys.exit(0)
     res = {}
-    for tag, env in (("host_sequenced", {"NEXR_LL_ASYNC": "0"}), ("queued_ticket_every_1", {"NEXR_LL_TICKET_EVERY": "1"}),
-                     ("queued_ticket_every_2", {"NEXR_LL_TICKET_EVERY": "2"}), ("queued_ticket_every_4", {}),
-                     ("queued_ticket_every_7", {"NEXR_LL_TICKET_EVERY": "7"})):
+    for tag, env in (("host_sequenced", {"NEXR_LL_ASYNC": "0"}),
+                     ("queued_ticket_every_4", {"NEXR_LL_RUN": "0"}), ("device_runs", {})):
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=dict(os.environ, **env),
                            capture_output=True, text=True, timeout=300)
         res[tag] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else p.stderr[-500:]
