@@ -313,13 +313,13 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
  * of them, as LLGenericOp<RECV=1> does) and nSend send FIFOs, each nSlots (NCCL_STEPS) slots of
  * slotBytes. recvStep[i] / sendStep[i] are the connection's step counters at the first step of the
  * run (the flags follow: NCCL_LL_FLAG(step + 1), :42-43); each recv / send step advances them by one.
- * Credits live in device memory, one 8-byte word per workgroup at a 64-B stride, NEXR_LL_HEAD_BYTES
- * per connection (zeroed when the connection is made): the receiver stores its step count into its
+ * Credits live in device memory, one 8-byte word per wave at a 16-B stride, NEXR_LL_HEAD_BYTES per
+ * connection (zeroed when the connection is made): the receiver stores its step count into its
  * connection's head words once it has read a step (postRecv), and a sender writes a slot only when
  * the head words of the connection it sends into show the step NCCL_STEPS earlier read (waitSend).
- * Both ends of a connection must therefore run their steps through this call (one workgroup of the
- * receiver's launch frees exactly the lines one workgroup of the sender's launch writes: both derive
- * the same grid from slotBytes). At the start of each launch the receiver stores recvStep into its
+ * Both ends of a connection must therefore run their steps through this call (one wave of the
+ * receiver's launch frees exactly the lines one wave of the sender's launch writes: both derive the
+ * same grid from slotBytes). At the start of each launch the receiver stores recvStep into its
  * head words, so a connection may switch to this call after steps run by nexrReduceCopyLL once those
  * have completed.
  *

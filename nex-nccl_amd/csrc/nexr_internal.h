@@ -51,11 +51,12 @@ struct LLParams {
 hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s);
 
 // A run of LL steps of one Primitives in one launch (nexrReduceCopyLLSteps; nexr_ll.hip). Workgroup w
-// owns line tiles t = w, w + grid, ... of every step (the same lines of every slot), so the credit of a
-// slot is per workgroup: head word w of a connection holds the steps receiver workgroup w has read.
+// owns line tiles t = w, w + grid, ... of every step and its wave v the same lines of each tile, on both
+// ends of a connection, so the credit of a slot is per wave: head word (w, v) of a connection holds the
+// steps the receiver's wave v of workgroup w has read.
 constexpr int kLLStepsMax = 96;        // steps per launch: the parameter block stays under 4 KiB
-constexpr int kLLHeadStride = 64;      // bytes between a connection's head words
-constexpr int kLLStepsMaxGrid = NEXR_LL_HEAD_BYTES / kLLHeadStride;
+constexpr int kLLHeadStride = 16;      // bytes between a connection's head words (one per wave)
+constexpr int kLLStepsMaxGrid = NEXR_LL_HEAD_BYTES / (kLLHeadStride * (kBlock / 64));
 struct LLStepsParams {
   const char* input;
   char* output;
@@ -71,6 +72,9 @@ struct LLStepsParams {
   uint64_t timeoutTicks;
   int nRecv, nSend, nSlots, nSteps;
   int firstWins;
+#ifdef NEXR_LL_STEPS_TRACE
+  uint64_t* trace;  // tuning harness only (tools/ll_steps_trace.hip)
+#endif
   nexrLLStep step[kLLStepsMax];
 };
 static_assert(sizeof(LLStepsParams) <= 4096, "kernel argument block");

@@ -12,6 +12,9 @@
 // kernel polls them with system-scope relaxed 64-bit loads, bounded in time, and reports a
 // timeout through the optional status word instead of hanging (checkAbort, primitives.h:142-156).
 //
+// A run of such steps in one launch, with waitSend / postRecv on device head words (nexrReduceCopyLLSteps,
+// reduce_copy_ll_steps_kernel below), and the LL128 step at the end of the file.
+//
 // MI355X mapping: one lane handles two lines 64 apart (one 16-byte data pack, so the LL path reuses
 // the SIMPLE path's per-datatype pack arithmetic, nexr_types.hpp, unchanged) and moves each line as
 // one 16-byte system-coherent access; a wave instruction covers 1 KiB of contiguous wire. Lines
@@ -55,26 +58,13 @@ __device__ __forceinline__ void wire_st(__amdgpu_buffer_rsrc_t r, uint32_t off, 
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreBits);
 }
 
-// Slow path: poll one LL line (16 bytes at p) until both flags equal `flag`; its 8 data bytes, or
-// false after the timeout (status set).
-template <typename A>
-__device__ __forceinline__ bool poll_line(const char* p, uint32_t flag, const A& a, uint64_t* data) {
-  uint64_t t0 = 0;
-  for (;;) {
-    const uint64_t w0 = ld_sys(p), w1 = ld_sys(p + 8);
-    if ((uint32_t)(w0 >> 32) == flag && (uint32_t)(w1 >> 32) == flag) {
-      *data = (uint32_t)w0 | (w1 << 32);
-      return true;
-    }
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (!t0) t0 = now;
-    else if (now - t0 > a.timeoutTicks) {
-      if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
+#ifndef NEXR_LL_CLOCK_EVERY  // overridable only by tuning harnesses (tools/ll_steps_trace.hip)
+#define NEXR_LL_CLOCK_EVERY 1
+#endif
+constexpr uint32_t kLLClockEvery = NEXR_LL_CLOCK_EVERY;
+#ifndef NEXR_LL_POLL_SLEEP  // the same: s_sleep between two tries of a line poll
+#define NEXR_LL_POLL_SLEEP 1
+#endif
 
 // The first n (<= 16) bytes at p as a zero-padded pack, and the reverse: byte accesses assembled in
 // registers (a variable-length memcpy into a register array would put the array on the stack).
@@ -135,14 +125,33 @@ __device__ __forceinline__ bool ll_tile(const A& a, uint64_t tile, uint64_t nByt
   u32x4 d[kLLU];
   bool ok[kLLU], two[kLLU];
   bool arrived = true;
+  // The first peer's lines are loaded before the user's: they wait for the peer (system-coherent, not
+  // cached), the user's only for memory, so the two latencies overlap. In a tile whose lines are all
+  // whole (every tile but a step's last) the user loads carry no per-line branch, so they go out
+  // together too instead of one after another.
+  u32x4 p0[kLLU], p1[kLLU];
+  if (a.nRecv > 0) {
+    const auto r = wire_rsrc(a.recv[0] + L0 * 16, (uint64_t)tileLines * 16);
+#pragma unroll
+    for (int u = 0; u < kLLU; u++) {  // past the end: zeros
+      p0[u] = wire_ld(r, (u * kLLSubLines + o0) * 16);
+      p1[u] = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
+    }
+  }
+  const bool wholeTile = (L0 + tileLines) * 8 <= nBytes;
 #pragma unroll
   for (int u = 0; u < kLLU; u++) {
     const uint32_t m0 = u * kLLSubLines + o0;
     ok[u] = m0 < tileLines;
     two[u] = m0 + 64 < tileLines;
     uint64_t s0 = 0, s1 = 0;
-    if (a.src && ok[u]) s0 = ld_line(a.src, L0 + m0, nBytes);
-    if (a.src && two[u]) s1 = ld_line(a.src, L0 + m0 + 64, nBytes);
+    if (a.src && wholeTile) {
+      if (ok[u]) s0 = *(const g_u64_a1*)(a.src + (L0 + m0) * 8);
+      if (two[u]) s1 = *(const g_u64_a1*)(a.src + (L0 + m0 + 64) * 8);
+    } else if (a.src) {
+      if (ok[u]) s0 = ld_line(a.src, L0 + m0, nBytes);
+      if (two[u]) s1 = ld_line(a.src, L0 + m0 + 64, nBytes);
+    }
     d[u] = (u32x4){(uint32_t)s0, (uint32_t)(s0 >> 32), (uint32_t)s1, (uint32_t)(s1 >> 32)};
     if constexpr (OP == nexrDevPreMulSum) {
       if (a.src && a.srcIsInput) d[u] = bc<u32x4>(T::mul(bc<V>(d[u]), T::splat(a.redArg)));  // applyPreOp
@@ -155,8 +164,8 @@ __device__ __forceinline__ bool ll_tile(const A& a, uint64_t tile, uint64_t nByt
     u32x4 x0[kLLU], x1[kLLU];
 #pragma unroll
     for (int u = 0; u < kLLU; u++) {  // past the end: zeros
-      x0[u] = wire_ld(r, (u * kLLSubLines + o0) * 16);
-      x1[u] = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
+      x0[u] = i == 0 ? p0[u] : wire_ld(r, (u * kLLSubLines + o0) * 16);
+      x1[u] = i == 0 ? p1[u] : wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
     }
     const uint32_t f = a.recvFlag[i];
 #pragma unroll
@@ -165,15 +174,30 @@ __device__ __forceinline__ bool ll_tile(const A& a, uint64_t tile, uint64_t nByt
       u32x4 peer;
       if (x0[u].y == f && x0[u].w == f && (!two[u] || (x1[u].y == f && x1[u].w == f))) {
         peer = (u32x4){x0[u].x, x0[u].z, x1[u].x, x1[u].z};
-      } else {  // not there yet: poll each line (readLL's loop, prims_ll.h:91-109)
-        const char* line = a.recv[i] + (L0 + u * kLLSubLines + o0) * 16;
-        uint64_t p0, p1 = 0;
-        if (!poll_line(line, f, a, &p0) || (two[u] && !poll_line(line + 64 * 16, f, a, &p1))) {
+      } else {  // not there yet: reload the lane's two lines until both carry the flag (readLL's loop,
+                // prims_ll.h:91-109), one 16-B access per line per try, bounded in time
+        uint64_t t0 = 0;
+        bool got = true;
+        for (uint32_t tries = 1;; tries++) {
+          if (NEXR_LL_POLL_SLEEP) __builtin_amdgcn_s_sleep(NEXR_LL_POLL_SLEEP);
+          x0[u] = wire_ld(r, (u * kLLSubLines + o0) * 16);
+          x1[u] = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
+          if (x0[u].y == f && x0[u].w == f && (!two[u] || (x1[u].y == f && x1[u].w == f))) break;
+          if (tries % kLLClockEvery) continue;  // the clock is a scalar memory read: not on every try
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (!t0) t0 = now;
+          else if (now - t0 > a.timeoutTicks) {
+            if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            got = false;
+            break;
+          }
+        }
+        if (!got) {
           ok[u] = false;  // never arrived: status set, this pack's outputs stay unwritten
           arrived = false;
           continue;
         }
-        peer = (u32x4){(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+        peer = (u32x4){x0[u].x, x0[u].z, x1[u].x, x1[u].z};
       }
       if ((i == 0 && !a.src) || a.firstWins) d[u] = peer;  // SKIP_COMP: applyReduce returns the peer
       else d[u] = bc<u32x4>(reduce_step<D, OP, IsMin>(bc<V>(peer), bc<V>(d[u])));  // applyReduce(op, peer, d)
@@ -265,24 +289,35 @@ hipError_t launch_ll(int dt, const LLParams& a, int op, int grid, hipStream_t s)
 // A run of LL steps in one launch (nexrReduceCopyLLSteps): LLGenericOp per step with the credit
 // protocol on the device (waitSend / postRecv, reference src/device/prims_ll.h:55-83). The reference
 // runs a step with one thread block and one head counter per connection; here a step's line tiles are
-// spread over the grid and every workgroup walks the steps on its own, so the credit is per workgroup:
-// workgroup w writes and reads the same line tiles of every slot (t = w, w + grid, ...) on both ends of a
-// connection, and head word w of the connection tells the sender's workgroup w how far the receiver's
-// workgroup w has read. No workgroup ever waits for another of its own launch.
+// spread over the grid, and inside a tile each wave owns its own lines (ll_tile: wave v, lines
+// [128v, 128v + 128) of every 512), the same lines of every slot on both ends of a connection. So the
+// credit is per wave: head word (w, v) of a connection tells the sender's wave v of workgroup w how far
+// the receiver's wave v of workgroup w has read, and every wave walks the steps on its own, with no
+// barrier: no wave ever waits for another wave of its own launch.
 // ---------------------------------------------------------------------------------------------
+constexpr int kLLWaves = kBlock / 64;
 __device__ __forceinline__ uint64_t* head_word(uint64_t* base, uint32_t w) {
-  return base + (size_t)w * (kLLHeadStride / 8);
+  return base + ((size_t)w * kLLWaves + (threadIdx.x >> 6)) * (kLLHeadStride / 8);
 }
-// waitSend's head poll (:58-62), bounded like the line polls.
-__device__ __forceinline__ bool wait_head(const uint64_t* p, uint64_t need, uint64_t timeoutTicks, uint32_t* status) {
+// waitSend's head poll (:58-62), by every lane of the wave on the same word (one request), bounded like
+// the line polls, into the wave's cache of the head (sendConnHeadCache): a fresh read only when the
+// cached value does not cover the step. Relaxed: the receiver published the head after its reads of the
+// slot were over (their values were in its outputs), and this wave's stores to the slot come after the
+// poll returned.
+__device__ __forceinline__ bool wait_head(const uint64_t* p, uint64_t need, uint64_t& cache, uint64_t timeoutTicks,
+                                          uint32_t* status) {
+  if (cache >= need) return true;
   uint64_t t0 = 0;
-  for (;;) {
-    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= need) return true;
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (!t0) t0 = now;
-    else if (now - t0 > timeoutTicks) {
-      if (status) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
+  for (uint32_t tries = 1;; tries++) {
+    cache = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (cache >= need) return true;
+    if (tries % kLLClockEvery == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (!t0) t0 = now;
+      else if (now - t0 > timeoutTicks) {
+        if (status) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
     }
     __builtin_amdgcn_s_sleep(1);
   }
@@ -304,40 +339,48 @@ struct LLStepArgs {  // the fields of LLParams that ll_tile reads, for one step 
 template <int D, int OP>
 __global__ __launch_bounds__(kBlock) void reduce_copy_ll_steps_kernel(LLStepsParams P) {
   constexpr uint64_t esz = 16 / Ty<D>::EPP;
-  __shared__ int sNoCredit;
-  const uint32_t w = blockIdx.x, G = gridDim.x;
-  uint64_t rs[NEXR_LL_STEPS_MAX_PEERS], ss[NEXR_LL_STEPS_MAX_PEERS];
-#pragma unroll
-  for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) rs[i] = P.recvStep[i], ss[i] = P.sendStep[i];
-  // Every earlier step of this stream has completed: whatever ran them, the slots before recvStep are read.
-  if (threadIdx.x == 0) {
-    sNoCredit = 0;
-    for (int i = 0; i < P.nRecv; i++)
-      __hip_atomic_store(head_word(P.recvHead[i], w), rs[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __syncthreads();
   constexpr int MP = NEXR_LL_STEPS_MAX_PEERS;
+  const uint32_t w = blockIdx.x, G = gridDim.x;
+  const bool lead = (threadIdx.x & 63) == 0;
+#ifdef NEXR_LL_STEPS_TRACE  // tuning harness only (tools/ll_steps_trace.hip): per-step phase times
+  __shared__ uint64_t tr[kLLStepsMax][5];
+#define NEXR_TRACE(k, j) \
+  if (threadIdx.x == 0) tr[k][j] = __builtin_amdgcn_s_memrealtime()
+#else
+#define NEXR_TRACE(k, j)
+#endif
+  // Step counters, their slot indices (kept by increment: a 64-bit modulo per step is a long scalar
+  // division) and the wave's cached heads.
+  uint64_t rs[MP], ss[MP], headCache[MP];
+  uint32_t rSlot[MP], sSlot[MP];
+#pragma unroll
+  for (int i = 0; i < MP; i++) {
+    rs[i] = P.recvStep[i], ss[i] = P.sendStep[i], headCache[i] = 0;
+    rSlot[i] = (uint32_t)(rs[i] % (uint64_t)P.nSlots), sSlot[i] = (uint32_t)(ss[i] % (uint64_t)P.nSlots);
+  }
+  // Every earlier step of this stream has completed: whatever ran them, the slots before recvStep are read.
+  if (lead)
+    for (int i = 0; i < P.nRecv; i++)
+      __hip_atomic_store(head_word(P.recvHead[i], w), rs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   LLStepArgs a;
   a.redArg = P.redArg;
   a.status = P.status;
   a.timeoutTicks = P.timeoutTicks;
   a.firstWins = P.firstWins;
   for (int k = 0; k < P.nSteps; k++) {
-    const nexrLLStep& st = P.step[k];
+    const nexrLLStep& st = P.step[k];  // scalar loads from the kernel arguments (an LDS copy was slower)
     const uint64_t nBytes = (uint64_t)st.nElts * esz;
     const uint64_t nLines = (nBytes + 7) / 8;
     const uint64_t nTiles = (nLines + kLLTileLines - 1) / kLLTileLines;
+    NEXR_TRACE(k, 0);
     if (w < nTiles) {
-      if (st.send) {  // waitSend: the receiver's workgroup w has read the step nSlots back
-        if (threadIdx.x == 0) {
-          for (int j = 0; j < P.nSend; j++)
-            if (ss[j] + 1 > (uint64_t)P.nSlots &&
-                !wait_head(head_word(const_cast<uint64_t*>(P.sendHead[j]), w), ss[j] + 1 - P.nSlots,
-                           P.timeoutTicks, P.status))
-              sNoCredit = 1;
-        }
-        __syncthreads();
-        if (sNoCredit) return;
+      if (st.send) {  // waitSend: the receiver's wave has read the step nSlots back
+#pragma unroll
+        for (int j = 0; j < MP; j++)
+          if (j < P.nSend && ss[j] + 1 > (uint64_t)P.nSlots &&
+              !wait_head(head_word(const_cast<uint64_t*>(P.sendHead[j]), w), ss[j] + 1 - P.nSlots, headCache[j],
+                         P.timeoutTicks, P.status))
+            return;  // no credit: status set, this wave stops
       }
       a.src = st.srcBuf == 0 ? P.input + st.srcIx * esz : st.srcBuf == 1 ? P.output + st.srcIx * esz : nullptr;
       a.dst = st.dstBuf == 0 ? const_cast<char*>(P.input) + st.dstIx * esz
@@ -346,13 +389,14 @@ __global__ __launch_bounds__(kBlock) void reduce_copy_ll_steps_kernel(LLStepsPar
       a.nSend = st.send ? P.nSend : 0;
 #pragma unroll
       for (int i = 0; i < MP; i++) {
-        a.recv[i] = P.recvFifo[i] + (rs[i] % P.nSlots) * P.slotBytes;
+        a.recv[i] = P.recvFifo[i] + (uint64_t)rSlot[i] * P.slotBytes;
         a.recvFlag[i] = (uint32_t)(rs[i] + 1);
-        a.send[i] = P.sendFifo[i] + (ss[i] % P.nSlots) * P.slotBytes;
+        a.send[i] = P.sendFifo[i] + (uint64_t)sSlot[i] * P.slotBytes;
         a.sendFlag[i] = (uint32_t)(ss[i] + 1);
       }
       a.srcIsInput = st.srcBuf == 0 && !P.firstWins;
       a.postOp = st.postOp && !P.firstWins;
+      NEXR_TRACE(k, 1);
       bool arrived = true;
       for (uint64_t t = w; t < nTiles; t += G) {
         if constexpr (OP == nexrDevMinMax) {
@@ -362,21 +406,38 @@ __global__ __launch_bounds__(kBlock) void reduce_copy_ll_steps_kernel(LLStepsPar
           arrived &= ll_tile<D, OP, false, LLStepArgs, MP>(a, t, nBytes, nLines);
         }
       }
-      if (__syncthreads_or(!arrived)) return;  // a line never came: status set, this workgroup stops
+      NEXR_TRACE(k, 2);
+      // a line never came: status set, this wave stops (its lines only; the other waves' are theirs)
+      if (__builtin_amdgcn_ballot_w64(!arrived)) return;
+      NEXR_TRACE(k, 3);
     }
-    if (st.recv) {  // postRecv: every lane's reads of the step are done (barrier), then the head
-      __syncthreads();
-      if (threadIdx.x == 0)
+    if (st.recv) {  // postRecv: the wave has used what it read of the step (its values are in the
+      // outputs), so the sender may rewrite those lines. Relaxed: a release would also wait for the
+      // outputs' own stores.
+      if (lead)
         for (int i = 0; i < P.nRecv; i++)
-          __hip_atomic_store(head_word(P.recvHead[i], w), rs[i] + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(head_word(P.recvHead[i], w), rs[i] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
-      for (int i = 0; i < NEXR_LL_STEPS_MAX_PEERS; i++) rs[i]++;
+      for (int i = 0; i < MP; i++) {
+        rs[i]++;
+        rSlot[i] = rSlot[i] + 1 == (uint32_t)P.nSlots ? 0 : rSlot[i] + 1;
+      }
     }
     if (st.send) {
 #pragma unroll
-      for (int j = 0; j < NEXR_LL_STEPS_MAX_PEERS; j++) ss[j]++;
+      for (int j = 0; j < MP; j++) {
+        ss[j]++;
+        sSlot[j] = sSlot[j] + 1 == (uint32_t)P.nSlots ? 0 : sSlot[j] + 1;
+      }
     }
+    NEXR_TRACE(k, 4);
   }
+#ifdef NEXR_LL_STEPS_TRACE
+  if (threadIdx.x == 0)
+    for (int k = 0; k < P.nSteps; k++)
+      for (int j = 0; j < 5; j++) P.trace[((size_t)w * kLLStepsMax + k) * 5 + j] = tr[k][j];
+#endif
+#undef NEXR_TRACE
 }
 
 template <int D>

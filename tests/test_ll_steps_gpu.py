@@ -103,10 +103,10 @@ def test_two_ranks_send_then_recv_reduce(nexr, dev, streams, slot_bytes, n_steps
     torch.cuda.synchronize()
     assert int(st_a.item()) == 0 and int(st_b.item()) == 0
     assert np.array_equal(out.cpu().numpy().view(np.uint32), (a + b).view(np.uint32))
-    # the receiver's head words: every workgroup has read every step
-    grid = min(64, -(-(slot_bytes // 16) // 512))
-    heads = _keep[slot_bytes * SLOTS:].view(torch.int64).cpu().numpy()[::8]
-    assert list(heads[:grid]) == [n_steps] * grid and not heads[grid:].any()
+    # the receiver's head words (one per wave at a 16-B stride): every wave has read every step
+    waves = 4 * min(64, -(-(slot_bytes // 16) // 512))
+    heads = _keep[slot_bytes * SLOTS:].view(torch.int64).cpu().numpy()[::2]
+    assert list(heads[:waves]) == [n_steps] * waves and not heads[waves:].any()
 
 
 def test_counters_carry_over_between_runs(nexr, dev, streams):
@@ -225,25 +225,28 @@ def test_a_missing_credit_ends_the_run_with_status(nexr, dev, streams):
 
 
 def test_overlapping_user_ranges_run_as_if_one_at_a_time(nexr, dev):
-    """Copies within the user buffers, no connections: step k copies output[k*s : k*s + n] to
-    output[(k+1)*s : (k+1)*s + n] with s < n, so every step reads what the one before wrote at another
-    position — the library starts a new launch for each; and 40 in-place scalings of one range
-    (the same range at the same position: one launch) — both exact against the sequential result."""
-    n, s = 5000, 1234
+    """Copies within the user buffers, no connections: step k reads output[P(k-1) + 13 : + n] and writes
+    output[P(k)] with P(k) = (k % 2) * 20000, so every step reads what the one before wrote at another
+    position (and writes what the one before that read at another position) — the library starts a new
+    launch for each; and 40 in-place scalings of one range (the same range at the same position: one
+    launch) — both exact against the sequential result."""
+    n, off, d = 5000, 20000, 13
     x = np.random.default_rng(3).integers(-100, 100, n).astype(np.float32)
-    total = n + 10 * s
+    total = 2 * off
     out = torch.zeros(total, dtype=torch.float32, device=dev)
     din = torch.from_numpy(x).to(dev)
     st = _status()
-    steps = [nexr.ll_step(0, 0, 1, 0, n)] + [nexr.ll_step(1, k * s, 1, (k + 1) * s, n) for k in range(10)]
+    steps = [nexr.ll_step(0, 0, 1, 0, n)] + [nexr.ll_step(1, ((k - 1) % 2) * off + d, 1, (k % 2) * off, n)
+                                             for k in range(1, 11)]
     torch.cuda.synchronize()
     nexr.reduce_copy_ll_steps(din.data_ptr(), out.data_ptr(), [], [], 1 << 16, steps, mg.F32, 0,
                               status=st.data_ptr())
     torch.cuda.synchronize()
     exp = np.zeros(total, np.float32)
     exp[:n] = x
-    for k in range(10):
-        exp[(k + 1) * s:(k + 1) * s + n] = exp[k * s:k * s + n].copy()
+    for k in range(1, 11):
+        src = ((k - 1) % 2) * off + d
+        exp[(k % 2) * off:(k % 2) * off + n] = exp[src:src + n].copy()
     assert np.array_equal(out.cpu().numpy(), exp)
     two = int(np.float32(2.0).view(np.uint32))
     y = torch.from_numpy(x.copy()).to(dev)
