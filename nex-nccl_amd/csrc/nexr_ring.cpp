@@ -332,8 +332,9 @@ nexrResult_t allocDone(uint32_t** w) {
 // a new stream takes the least used one), and two streams on one queue run their kernels one after the
 // other, so a run waiting for its peer's would end only at its timeout. A stream made with a CU mask gets a
 // hardware queue of its own (the runtime does not share those); with every CU in the mask it runs like any
-// other stream (tools/ll_run_queue_probe.py). Device-memory communicators make their rank streams so
-// (NEXR_RING_OWN_QUEUES=0: plain streams, and no device runs); *own reports whether it worked.
+// other stream (tools/ll_run_queue_probe.py). Device-memory LL communicators, the ones whose steps may
+// run so, make their rank streams that way (NEXR_RING_OWN_QUEUES=0: plain streams, and no device runs);
+// *own reports whether it worked.
 hipError_t createRankStream(const nexrRingComm* c, hipStream_t* s, bool* own) {
   static const bool off = [] {
     const char* e = getenv("NEXR_RING_OWN_QUEUES");
@@ -341,7 +342,7 @@ hipError_t createRankStream(const nexrRingComm* c, hipStream_t* s, bool* own) {
   }();
   *own = false;
   int dev = 0, cus = 0;
-  if (c->cfg.memMode == nexrRingDeviceMemory && !off && hipGetDevice(&dev) == hipSuccess &&
+  if (c->cfg.memMode == nexrRingDeviceMemory && c->proto == nexrRingProtoLL && !off && hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
     std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
     if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
