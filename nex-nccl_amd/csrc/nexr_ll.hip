@@ -62,6 +62,9 @@ __device__ __forceinline__ void wire_st(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 #define NEXR_LL_CLOCK_EVERY 1
 #endif
 constexpr uint32_t kLLClockEvery = NEXR_LL_CLOCK_EVERY;
+#ifndef NEXR_LL_POLL_PIPE  // the same: two tries of a line poll in flight (1) or one (0)
+#define NEXR_LL_POLL_PIPE 0
+#endif
 #ifndef NEXR_LL_POLL_SLEEP  // the same: s_sleep between two tries of a line poll
 #define NEXR_LL_POLL_SLEEP 1
 #endif
@@ -178,10 +181,21 @@ __device__ __forceinline__ bool ll_tile(const A& a, uint64_t tile, uint64_t nByt
                 // prims_ll.h:91-109), one 16-B access per line per try, bounded in time
         uint64_t t0 = 0;
         bool got = true;
+#if NEXR_LL_POLL_PIPE
+        // Two tries in flight: the next one is issued before the current one is looked at, so a line that
+        // lands while a try is on its way is seen one sleep later rather than one round trip later.
+        u32x4 n0 = wire_ld(r, (u * kLLSubLines + o0) * 16), n1 = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
+#endif
         for (uint32_t tries = 1;; tries++) {
           if (NEXR_LL_POLL_SLEEP) __builtin_amdgcn_s_sleep(NEXR_LL_POLL_SLEEP);
+#if NEXR_LL_POLL_PIPE
+          x0[u] = n0, x1[u] = n1;
+          n0 = wire_ld(r, (u * kLLSubLines + o0) * 16);
+          n1 = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
+#else
           x0[u] = wire_ld(r, (u * kLLSubLines + o0) * 16);
           x1[u] = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
+#endif
           if (x0[u].y == f && x0[u].w == f && (!two[u] || (x1[u].y == f && x1[u].w == f))) break;
           if (tries % kLLClockEvery) continue;  // the clock is a scalar memory read: not on every try
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
