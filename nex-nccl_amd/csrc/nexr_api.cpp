@@ -147,12 +147,14 @@ void llSemantics(int* dt, int* op, int* srcIsInput, int* postOp, int* firstWins)
 // sweeps. The workgroup geometry follows the policy (unroll_for/block_for, nexr_internal.h).
 // One exception (round 5): calls with few sources take nt stores as well from
 // NEXR_NT_STORE_K2_MIN_BYTES (96 MiB streamed), for the (K, M) measured to gain at 96-510 MiB
-// (tools/occupancy_ab.hip ntstore / ntstore2 / ntstore3 / c4pol): K = 1 with M = 1-4 (1.1-4.8 %),
-// K = 2 with M = 1-6 (2.2-6.3 %), K = 3 with M = 2-5 (3.1-5.6 %) (profiles/r05q_occupancy_ntstore.txt,
-// r05zd_occupancy_ntstore2.txt, r05zg_occupancy_ntstore3.txt, r05zj_occupancy_ntstore3_m5.txt). Outside
-// it nt stores were mixed (K = 3 M = 1, K = 1 M = 5) or lost (K = 1 M = 8: 2.9-5.9 %, K = 4 M = 2,
-// K = 8). nDsts = 0: unknown (a batch), the general rule.
-constexpr int kNtStoreMinM[4] = {0, 1, 1, 2}, kNtStoreMaxM[4] = {0, 4, 6, 5};
+// (tools/occupancy_ab.hip ntstore / ntstore2 / ntstore3 / c4pol / ntstore4): K = 1 with M = 1-4
+// (1.1-4.8 %), K = 2 with M = 1-7 (2.2-6.3 %; M = 7, round 6: 0.7-2.4 %), K = 3 with M = 2-7 (3.1-5.6 %;
+// M = 6-7, round 6: 0-5.0 %, never slower) (profiles/r05q_occupancy_ntstore.txt,
+// r05zd_occupancy_ntstore2.txt, r05zg_occupancy_ntstore3.txt, r05zj_occupancy_ntstore3_m5.txt,
+// r06w_occupancy_ntstore4.txt). Outside it nt stores were mixed (K = 3 M = 1, K = 1 M = 5, K = 2 M = 8
+// and K = 3 M = 8: 1.3-4.8 % slower at 110-120 MiB, 2.3-4.7 % faster at 290-300) or lost (K = 1 M = 8:
+// 2.9-5.9 %, K = 4 M = 2, K = 8). nDsts = 0: unknown (a batch), the general rule.
+constexpr int kNtStoreMinM[4] = {0, 1, 1, 2}, kNtStoreMaxM[4] = {0, 4, 7, 7};
 int pickPolicy(uint64_t streamBytes, int nSrcs = 0, int nDsts = 0) {
   static const long polOverride = envLong("NEXR_POLICY", -1);
   static const long ntLoadMin = envLong("NEXR_NT_LOAD_MIN_BYTES", 64l << 20);

@@ -234,9 +234,9 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
                            (8, 9, 1 << 20, (128, 1024, 1, 0)), (8, 6, 8 << 20, (1024, 1024, 1, 1))):
         info = nexr.query_launch(k8[:k], [0x90000000], n, dt)
         assert (info.grid, info.block, info.packsPerLane, info.policy) == want, (k, dt, n)
-    # K = 1 with M = 1-4, K = 2 with M = 1-6 and K = 3 with M = 2-5 take nt stores from 96 MiB streamed
-    # (round 5); K = 3 with one destination, K = 1 with M >= 5, K >= 4 the general rule (nt loads from
-    # 64 MiB, nt stores from 512)
+    # K = 1 with M = 1-4, K = 2 with M = 1-7 and K = 3 with M = 2-7 take nt stores from 96 MiB streamed
+    # (rounds 5-6); K = 3 with one destination, K = 1 with M >= 5, K = 2-3 with M = 8, K >= 4 the general
+    # rule (nt loads from 64 MiB, nt stores from 512)
     d2, d3 = [0x90000000, 0xa0000000], [0x90000000, 0xa0000000, 0xb0000000]
     d5 = [0x90000000 + 0x10000000 * i for i in range(5)]
     for srcs_, dsts_, mib, want_pol in ((k8[:2], [0x90000000], 8, 0), (k8[:2], [0x90000000], 32, 3),
@@ -245,7 +245,8 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
                                          (k8[:1], [0x90000000], 32, 1), (k8[:1], d2, 32, 3), (k8[:2], d3, 32, 3),
                                          (k8[:1], d5[:4], 20, 3), (k8[:3], d2, 20, 3), (k8[:3], d3, 16, 3),
                                          (k8[:4], d2, 16, 1), (k8[:2], d5, 16, 3), (k8[:1], d5, 20, 1),
-                                         (k8[:3], d5, 12, 3), (k8[:2], d5 + d2, 12, 1), (k8[:3], d5 + d2[:1], 12, 1)):
+                                         (k8[:3], d5, 12, 3), (k8[:2], d5 + d2, 12, 3), (k8[:3], d5 + d2[:1], 12, 3),
+                                         (k8[:3], d5 + d2, 12, 3), (k8[:2], d5 + d3, 12, 1), (k8[:3], d5 + d3, 12, 1)):
         info = nexr.query_launch(srcs_, dsts_, (mib << 20) // 4, 7)
         assert info.policy == want_pol, (len(srcs_), len(dsts_), mib)
     # head/body/tail split for a shared 4-B phase: the head brings dst0 to its next 128-B boundary
@@ -272,10 +273,10 @@ def test_query_launch_grid_respects_the_work_item_limit(nexr):
 
 def test_nt_store_table_at_its_threshold(nexr):
     """pickPolicy's (K, M) table (nexr_api.cpp, round 5): every K = 1..8 x M = 1..8 just at and just
-    below 96 MiB streamed. Inside the table (K = 1 with M = 1-4, K = 2 with M = 1-6, K = 3 with M = 2-5)
+    below 96 MiB streamed. Inside the table (K = 1 with M = 1-4, K = 2 with M = 1-7, K = 3 with M = 2-7)
     the call takes nt loads + stores (3) from 96 MiB; everywhere else, and below 96 MiB, the general
     rule's nt loads (1) between 64 and 512 MiB."""
-    table = {1: range(1, 5), 2: range(1, 7), 3: range(2, 6)}
+    table = {1: range(1, 5), 2: range(1, 8), 3: range(2, 8)}
     mib96 = 96 << 20
     for k in range(1, 9):
         for m in range(1, 9):

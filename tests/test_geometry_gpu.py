@@ -206,7 +206,8 @@ def _run_m(nexr, srcs, m, dt, op, arg, offs):
 @pytest.mark.parametrize("dt,k,m,op,name,buf_mib", [(mg.F32, 1, 1, mg.SUM, "sum", 49), (mg.I8, 1, 2, mg.MINMAX, "max", 33),
                                                     (mg.F32, 2, 2, mg.SUM, "sum", 25), (mg.BF16, 2, 2, mg.PROD, "prod", 26),
                                                     (mg.F16, 1, 4, mg.SUM, "sum", 20), (mg.I32, 3, 2, mg.MINMAX, "min", 20),
-                                                    (mg.F32, 2, 6, mg.SUM, "sum", 13), (mg.U8, 3, 5, mg.MINMAX, "max", 13)])
+                                                    (mg.F32, 2, 6, mg.SUM, "sum", 13), (mg.U8, 3, 5, mg.MINMAX, "max", 13),
+                                                    (mg.F32, 2, 7, mg.SUM, "sum", 11), (mg.BF16, 3, 7, mg.SUM, "sum", 10)])
 def test_small_fan_in_nt_store_policy_edges(nexr, oracle, dev, dt, k, m, op, name, buf_mib):
     """Copies (K = 1), the ring's two-destination steps and the tree's K = 1 M = 4 / K = 3 M = 2 steps
     just past 96 MiB streamed launch the nt-store policy at the default 4 x 256 shape; whole trips, a remainder plus edges, and mixed 16-B phases

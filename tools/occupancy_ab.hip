@@ -262,6 +262,26 @@ int main(int argc, char** argv) {
       cfgs.push_back({name, c.k, (size_t)c.mib << 20, fin, v, c.m});
     }
   }
+  if (group == "ntstore4") {  // round 6: K = 2 with M = 7-8, K = 3 with M = 6-8 at 100-510 MiB streamed,
+                               // and K = 5-8 (M = 1) just below the 512 MiB nt-store threshold
+    constexpr int D = nexrFloat32, OP = nexrDevSum;
+    struct KM { int k, m, mib; };
+    const std::vector<KM> shapes = {KM{2, 7, 12}, KM{2, 7, 32}, KM{2, 7, 56}, KM{2, 8, 12}, KM{2, 8, 30}, KM{2, 8, 50},
+                                    KM{3, 6, 12}, KM{3, 6, 32}, KM{3, 6, 56}, KM{3, 7, 11}, KM{3, 7, 30},
+                                    KM{3, 7, 50}, KM{3, 8, 10}, KM{3, 8, 26}, KM{3, 8, 46}, KM{5, 1, 80},
+                                    KM{5, 1, 85}, KM{6, 1, 69}, KM{6, 1, 73}, KM{8, 1, 53}, KM{8, 1, 56}};
+    for (KM c : shapes) {
+      char* name = new char[96];
+      snprintf(name, 96, "fp32 sum K=%d M=%d %d MiB (%d MiB streamed)", c.k, c.m, c.mib, (c.k + c.m) * c.mib);
+      std::vector<Var> v;
+#define NT4(K)                                                                                           \
+  v = {var<D, OP, K, kPolNtLoad, false, unroll_for(D, K, kPolNtLoad), block_for(D, K, kPolNtLoad)>("nt-ld", 0), \
+       var<D, OP, K, kPolNt, false, unroll_for(D, K, kPolNt), block_for(D, K, kPolNt)>("nt-st", lds_for(D, K, kPolNt) ? 1 : 0)};
+      if (c.k == 2) { NT4(2) } else if (c.k == 3) { NT4(3) } else if (c.k == 5) { NT4(5) } else if (c.k == 6) { NT4(6) } else { NT4(8) }
+#undef NT4
+      cfgs.push_back({name, c.k, (size_t)c.mib << 20, fin, v, c.m});
+    }
+  }
   if (group == "c3pol") {  // C3 (K = 8, 256 MiB per buffer, 2.25 GiB streamed) and C2: nt stores or nt loads only
     {
       constexpr int D = nexrFloat16, OP = nexrDevSum, K = 8;
