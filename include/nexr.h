@@ -277,7 +277,9 @@ typedef struct {
  *   sendLines[i] = {lo32(d), flag_i, hi32(d), flag_i};  dst = d  (valid elements only)
  * Recv lines are polled until both flags match (system-scope loads), for at most timeoutUs
  * (0 = 1 s); a line that never becomes valid sets *status = 1 (status: optional device/host-mapped
- * word) and its outputs are left unwritten — the kernel never hangs. src/dst are any-aligned device
+ * word) and its outputs are left unwritten — the kernel never hangs. A poll that keeps failing also
+ * reads *status every 64 tries and gives up when it is non-zero (another step timed out, or the
+ * caller wrote it to abort: checkAbort, primitives.h:142-156). src/dst are any-aligned device
  * pointers (nullable: at least one input and one output); line buffers must be 16-B aligned.
  */
 NEXR_API nexrResult_t nexrReduceCopyLL(const void* src, int srcIsInput, int nRecv, const void* const* recvLines,
@@ -328,7 +330,8 @@ NEXR_API nexrResult_t nexrReduceCopyLL128(const void* src, int srcIsInput, int n
  * one at a time in order: where a step reads or writes user bytes an earlier step of the same launch
  * wrote or read at a different element position, the library starts a new launch. A step whose line
  * never arrives (or whose credit never comes) within timeoutUs sets *status = 1 and ends its
- * workgroup's run; the launch never hangs. Launches are stream-ordered; the call returns after
+ * wave's run, and a non-zero *status ends the others' polls early (as nexrReduceCopyLL); the launch
+ * never hangs. Launches are stream-ordered; the call returns after
  * queueing them. The runs on both ends of a connection must be able to run at once: streams on
  * hardware queues of their own (HIP shares its GPU_MAX_HW_QUEUES queues among streams and runs one
  * queue's kernels one after the other; a stream made by hipExtStreamCreateWithCUMask has its own), and

@@ -473,17 +473,45 @@ struct Prims {
     return true;
   }
   // The end of a collective run on the device: the last launch queued, the stream complete, then the
-  // host counters (which host-sequenced collectives read) published as if every step had posted.
+  // host counters (which host-sequenced collectives read) published as if every step had posted. When
+  // another rank has failed, the steps not yet launched are dropped and the abort is relayed into this
+  // rank's status word, which the run's polls read now and then (nexr_ll.hip): its kernels end at once
+  // instead of at their timeout (checkAbort, primitives.h:142-156).
   bool finishRun() {
     llRun = false;
-    bool ok = flushRun();
-    if (!streamDone()) {
+    bool ok;
+    if (sh->aborted()) {
+      run.clear();
+      __atomic_store_n(status, 2u, __ATOMIC_RELEASE);
+      ok = false;
+    } else {
+      ok = flushRun();
+    }
+    const uint32_t t = ++done[1];
+    bool landed = false;
+    if (hipStreamWriteValue32(stream, done, t, 0) == hipSuccess) {
+      const int timeoutMs = c->cfg.timeoutMs > 0 ? c->cfg.timeoutMs : 60000;
+      auto t0 = std::chrono::steady_clock::now();
+      for (unsigned spins = 0;; spins++) {
+        if ((int32_t)(__atomic_load_n(done, __ATOMIC_ACQUIRE) - t) >= 0) {
+          landed = true;
+          break;
+        }
+        if (sh->aborted() && __atomic_load_n(status, __ATOMIC_ACQUIRE) == 0)
+          __atomic_store_n(status, 2u, __ATOMIC_RELEASE);
+        if ((spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs))
+          break;
+        if (spins >= 4096) std::this_thread::yield();
+      }
+    }
+    if (!landed && hipStreamSynchronize(stream) != hipSuccess) {
       sh->fail(nexrUnhandledCudaError);
       ok = false;
     }
     for (int i = 0; i < nRecv; i++) recv[i]->st->head.store(recv[i]->recvStep, std::memory_order_release);
     for (int i = 0; i < nSend; i++) send[i]->st->tail.store(send[i]->sendStep, std::memory_order_release);
-    if (ok && __atomic_load_n(status, __ATOMIC_ACQUIRE) != 0) {
+    const uint32_t st = __atomic_load_n(status, __ATOMIC_ACQUIRE);
+    if (ok && st != 0) {
       sh->fail(nexrInternalError);
       ok = false;
     }

@@ -62,6 +62,13 @@ __device__ __forceinline__ void wire_st(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 #define NEXR_LL_CLOCK_EVERY 1
 #endif
 constexpr uint32_t kLLClockEvery = NEXR_LL_CLOCK_EVERY;
+// A poll that keeps failing also reads the status word now and then (every kLLAbortEvery tries, a read
+// over PCIe when the word is pinned host memory): non-zero means another step timed out or the caller
+// aborted (checkAbort, primitives.h:142-156), and the poll gives up at once instead of at its timeout.
+constexpr uint32_t kLLAbortEvery = 64;
+__device__ __forceinline__ bool ll_aborted(const uint32_t* status) {
+  return status && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
 #ifndef NEXR_LL_POLL_PIPE  // the same: two tries of a line poll in flight (1) or one (0)
 #define NEXR_LL_POLL_PIPE 0
 #endif
@@ -197,6 +204,10 @@ __device__ __forceinline__ bool ll_tile(const A& a, uint64_t tile, uint64_t nByt
           x1[u] = wire_ld(r, (u * kLLSubLines + o0 + 64) * 16);
 #endif
           if (x0[u].y == f && x0[u].w == f && (!two[u] || (x1[u].y == f && x1[u].w == f))) break;
+          if (tries % kLLAbortEvery == 0 && ll_aborted(a.status)) {  // checkAbort (primitives.h:142-156)
+            got = false;
+            break;
+          }
           if (tries % kLLClockEvery) continue;  // the clock is a scalar memory read: not on every try
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (!t0) t0 = now;
@@ -325,6 +336,7 @@ __device__ __forceinline__ bool wait_head(const uint64_t* p, uint64_t need, uint
   for (uint32_t tries = 1;; tries++) {
     cache = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (cache >= need) return true;
+    if (tries % kLLAbortEvery == 0 && ll_aborted(status)) return false;
     if (tries % kLLClockEvery == 0) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (!t0) t0 = now;

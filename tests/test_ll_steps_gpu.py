@@ -257,3 +257,27 @@ def test_overlapping_user_ranges_run_as_if_one_at_a_time(nexr, dev):
     torch.cuda.synchronize()
     assert int(st.item()) == 0
     assert np.array_equal(y.cpu().numpy(), x * np.float32(2.0 ** 40))
+
+
+def test_a_host_abort_ends_the_run(nexr, dev, streams):
+    """The status word as an abort flag (checkAbort, primitives.h:142-156): a run waiting for lines that
+    never come, with a 10 s timeout, ends soon after the host writes 2 into its (pinned, device-mapped)
+    status word — the ring's rank threads relay another rank's failure this way."""
+    import time
+    slot = 1 << 16
+    per = slot // 8
+    _keep, fifo, head = _conn(slot)
+    x = torch.ones(20 * per, dtype=torch.float32, device=dev)
+    out = torch.zeros_like(x)
+    st = torch.zeros(1, dtype=torch.int32).pin_memory()
+    (s,) = streams(1)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    nexr.reduce_copy_ll_steps(x.data_ptr(), out.data_ptr(), [(fifo, head, 0)], [], slot,
+                              [nexr.ll_step(0, k * per, 1, k * per, per, recv=True) for k in range(20)], mg.F32, 0,
+                              status=st.data_ptr(), timeout_us=10_000_000, stream=s)
+    time.sleep(0.2)
+    st[0] = 2
+    torch.cuda.synchronize()
+    assert time.time() - t0 < 3.0
+    assert int(st[0]) == 2 and not out.any()
