@@ -575,6 +575,15 @@ def test_multi_device_c_example_builds(monkeypatch):
     assert os.path.exists(exe) and os.access(exe, os.X_OK)
 
 
+def test_ll_steps_c_example_builds():
+    """examples/ll_steps_c.c (a run of LL steps with device credits from plain C through
+    nexrReduceCopyLLSteps, streams from hipExtStreamCreateWithCUMask) compiles and links with gcc
+    -std=c11 -Wall -Wextra -Werror."""
+    import __graft_entry__
+    exe = __graft_entry__.build_c_ll_steps()
+    assert os.path.exists(exe) and os.access(exe, os.X_OK)
+
+
 def test_hip_runtime_is_the_one_libnexr_uses(nexr):
     """nexr.hip_runtime() hands back the single mapped libamdhip64 (harness calls such as
     hipDeviceEnablePeerAccess must reach the runtime the kernels launch on)."""

@@ -31,3 +31,16 @@ def test_c_multi_device_program(args):
     p = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "multi_device_c ok" in p.stdout, p.stdout + p.stderr
     print(p.stdout.strip())
+
+
+@pytest.mark.parametrize("args", [("40", "64"), ("100", "4"), ("9", "1024")])
+def test_c_ll_steps_program(args):
+    """A run of LL steps with device credits from plain C (nexrReduceCopyLLSteps): 40 steps through 8
+    slots of 64 KiB, 100 through 4 KiB slots (one workgroup), 9 through 1 MiB slots (64 workgroups, two
+    tiles each); every output element checked against a + b on the host."""
+    exe = os.path.join(ROOT, "xbin", "ll_steps_c")
+    if not os.path.exists(exe):
+        import __graft_entry__
+        exe = __graft_entry__.build_c_ll_steps()
+    p = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "ll_steps_c ok" in p.stdout, p.stdout + p.stderr
