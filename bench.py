@@ -429,6 +429,7 @@ def c1_ring(iters: int = 20) -> dict:
                     comm.all_reduce(sp, rp, count, 7, 0)
                 dt = (time.perf_counter() - t0) / reps
                 hp = nexr.host_path_stats(reset=True)
+                ll_mode = comm.queued()
         finally:
             for h in handles:
                 nexr.host_deregister(h)
@@ -445,6 +446,9 @@ def c1_ring(iters: int = 20) -> dict:
                 **{f"{k}_us": round(hp[k + "Ns"] / steps / 1e3, 2) for k in ("classify", "copy", "launch", "wait")}}
         if mode == ring.DEVICE_MEMORY:
             out[name]["step_wait"] = wait  # "word" with both ranks on one GPU, "sync" across GPUs
+        if proto == ring.PROTO_LL:
+            # how the LL steps ran (nexrRingCommGetQueued): device runs / queued / host-sequenced
+            out[name]["ll_steps"] = {2: "device runs", 1: "queued launches", 0: "host-sequenced"}.get(ll_mode, ll_mode)
     out["note"] = ("plumbing, not a roofline config (SURVEY §8(d) C1); device_ll / device_ll128 run the same ring "
                    "with the LL / LL128 protocol steps (SURVEY §8(f) #3) in place of SIMPLE; cpu_oracle runs the same schedule with the "
                    "reference's CPU execution of reduceCopy (oracle_reduce_copy_emulated_fn: 480 emulated threads, "
