@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                \
@@ -35,6 +36,10 @@ int main() {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+  // LL_TRACE_MASK (A/B of placement): "full" (default), "same" (both ranks on logical CUs 0-31),
+  // "split" (rank 0 on 0-31, rank 1 on 32-63)
+  const char* mm = getenv("LL_TRACE_MASK");
+  const std::string maskMode = mm ? mm : "full";
   hipStream_t st[2];
   char *in[2], *out[2], *fifo[2];
   uint64_t* tr[2];
@@ -42,7 +47,12 @@ int main() {
   CK(hipHostMalloc((void**)&status, 64, hipHostMallocMapped));
   memset(status, 0, 64);
   for (int r = 0; r < nRanks; r++) {
-    CK(hipExtStreamCreateWithCUMask(&st[r], (uint32_t)mask.size(), mask.data()));
+    std::vector<uint32_t> m = mask;
+    if (maskMode != "full") {
+      for (auto& x : m) x = 0;
+      m[maskMode == "split" ? r : 0] = 0xffffffffu;
+    }
+    CK(hipExtStreamCreateWithCUMask(&st[r], (uint32_t)m.size(), m.data()));
     CK(hipMalloc((void**)&in[r], count * 4));
     CK(hipMalloc((void**)&out[r], count * 4));
     CK(hipMalloc((void**)&fifo[r], slot * slots + NEXR_LL_HEAD_BYTES));  // FIFO INTO rank r
